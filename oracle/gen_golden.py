@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""oracle/gen_golden.py -- TEST INFRASTRUCTURE ONLY: regenerate tests/golden/*.npz.
+
+Runs oracle/_ref/ref_harness (the reference's own BVH / triangle / material / camera / OBJ-loader
+code compiled from /root/reference by `make -C oracle ref`) on seeded synthetic inputs and stores
+inputs + outputs as small .npz fixtures.  Only data is stored: no reference source text.
+Container-only (needs /root/reference); the GPU box uses the committed fixtures.
+
+    python oracle/gen_golden.py            # all fixtures
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+GOLDEN = os.path.join(REPO, "tests", "golden")
+HARNESS = os.path.join(HERE, "_ref", "ref_harness")
+REF = os.environ.get("RT_REFERENCE", "/root/reference")
+CORNELL_DIR = os.path.join(REF, "Monte Carlo Path Tracer", "8599RayTracerGUI", "src", "cornellbox")
+MESH_NAMES = ["floor", "shortbox", "tallbox", "left", "right", "light"]
+# Renderer::Renderer materials, MC/Renderer.cpp:28-41 (red, green, white, light)
+ALBEDO = np.array([[0.63, 0.065, 0.05], [0.1, 0.5, 0.1], [0.7, 0.7, 0.7], [0.7, 0.7, 0.7]], np.float32)
+EMISSION = np.array([[0, 0, 0], [0, 0, 0], [0, 0, 0], [47.8, 38.6, 31.1]], np.float32)
+MESH_MATERIAL = [2, 2, 2, 0, 1, 3]
+
+NODE_DT = np.dtype([("mn", "<f4", 3), ("mx", "<f4", 3), ("area", "<f4"), ("left", "<i4"), ("right", "<i4"),
+                    ("tri", "<i4"), ("mesh", "<i4"), ("top", "<i4")])
+TRI_DT = np.dtype([("a", "<f4", 3), ("b", "<f4", 3), ("c", "<f4", 3), ("n", "<f4", 3), ("area", "<f4"),
+                   ("mesh", "<i4"), ("material", "<i4")])
+MESH_DT = np.dtype([("total_area", "<f4"), ("mn", "<f4", 3), ("mx", "<f4", 3), ("material", "<i4"), ("emissive", "<i4")])
+HIT_DT = np.dtype([("hit", "<i4"), ("tri", "<i4"), ("mat", "<i4"), ("t", "<f8"), ("loc", "<f4", 3), ("n", "<f4", 3)])
+
+
+def run(*args):
+    r = subprocess.run([HARNESS] + [str(a) for a in args], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"harness {args[0]} failed: {r.returncode} {r.stderr}")
+    print(" ", r.stdout.strip())
+
+
+def tmp(name):
+    return os.path.join(TMP, name)
+
+
+def gen_scene():
+    raw = {}
+    for n in MESH_NAMES:
+        run("objraw", os.path.join(CORNELL_DIR, n + ".obj"), tmp(n + ".raw"))
+        raw[n] = np.fromfile(tmp(n + ".raw"), "<f4").reshape(-1, 9)
+    run("scene", CORNELL_DIR, "", tmp("nodes"), tmp("tris"), tmp("meshes"))
+    nodes = np.fromfile(tmp("nodes"), NODE_DT)
+    tris = np.fromfile(tmp("tris"), TRI_DT)
+    meshes = np.fromfile(tmp("meshes"), MESH_DT)
+    out = {f"raw_{n}": raw[n] for n in MESH_NAMES}
+    out.update(albedo=ALBEDO, emission=EMISSION, mesh_material=np.array(MESH_MATERIAL, np.int32),
+               nodes=nodes.view(np.uint8), tris=tris.view(np.uint8), meshes=meshes.view(np.uint8))
+    np.savez_compressed(os.path.join(GOLDEN, "cornell_scene.npz"), **out)
+    return tris
+
+
+def gen_rays(tris, rng):
+    n = 4096
+    cam = np.array([2.81432, 4.20749, -9.11751], np.float32)
+    lo, hi = np.array([0, 0, 0], np.float32), np.array([5.56, 5.488, 5.592], np.float32)
+    o, d = [], []
+    # (a) camera rays towards random points of the box
+    k = 1200
+    tgt = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    o.append(np.repeat(cam[None], k, 0)); d.append(tgt - cam)
+    # (b) random interior origins, random directions
+    k = 1200
+    o.append(rng.uniform(lo, hi, (k, 3)).astype(np.float32)); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    # (c) axis-aligned / signed-zero directions (slab NaN / inf paths)
+    k = 600
+    oo = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    dd = np.zeros((k, 3), np.float32)
+    ax = rng.integers(0, 3, k)
+    dd[np.arange(k), ax] = rng.choice([-1.0, 1.0], k)
+    negz = rng.random((k, 3)) < 0.5
+    dd = np.where((dd == 0) & negz, np.float32(-0.0), dd)
+    o.append(oo); d.append(dd)
+    # (d) origins exactly on walls / light plane / box tops
+    k = 500
+    oo = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    which = rng.integers(0, 4, k)
+    oo[which == 0, 1] = 0.0
+    oo[which == 1, 1] = np.float32(5.487)
+    oo[which == 2, 0] = 0.0
+    oo[which == 3, 2] = np.float32(5.592)
+    o.append(oo); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    # (e) towards triangle vertices and edge midpoints (shared-edge / tie cases)
+    k = n - sum(len(x) for x in o)
+    ti = rng.integers(0, len(tris), k)
+    w = rng.integers(0, 4, k)
+    a, b, c = tris["a"][ti], tris["b"][ti], tris["c"][ti]
+    tgt = np.where((w == 0)[:, None], a, np.where((w == 1)[:, None], b, np.where((w == 2)[:, None], 0.5 * (a + b), 0.5 * (b + c))))
+    src = np.where((rng.random(k) < 0.5)[:, None], cam[None], rng.uniform(lo, hi, (k, 3)).astype(np.float32))
+    o.append(src.astype(np.float32)); d.append((tgt - src).astype(np.float32))
+    o = np.concatenate(o).astype(np.float32)
+    d = np.concatenate(d).astype(np.float32)
+    np.concatenate([o, d], 1).astype("<f4").tofile(tmp("rays.in"))
+    run("rays", CORNELL_DIR, "", tmp("rays.in"), tmp("rays.out"))
+    res = np.fromfile(tmp("rays.out"), HIT_DT)
+    np.savez_compressed(os.path.join(GOLDEN, "rays_cornell.npz"), org=o, dir=d, hit=res["hit"], tri=res["tri"],
+                        mat=res["mat"], t=res["t"], loc=res["loc"], n=res["n"])
+
+
+def gen_mt(rng):
+    cases = []
+    k = 3000
+    v = rng.normal(size=(k, 3, 3)).astype(np.float32)
+    org = rng.normal(size=(k, 3)).astype(np.float32) * 3
+    tgt = (v.mean(1) + rng.normal(size=(k, 3)) * 0.6).astype(np.float32)
+    cases.append(np.concatenate([v.reshape(k, 9), org, tgt - org], 1))
+    # degenerate triangles, parallel rays, rays through vertices/edges, zero direction
+    k = 600
+    v = rng.normal(size=(k, 3, 3)).astype(np.float32)
+    v[:200, 2] = v[:200, 1]                       # zero area
+    org = rng.normal(size=(k, 3)).astype(np.float32) * 3
+    d = rng.normal(size=(k, 3)).astype(np.float32)
+    e1 = v[:, 1] - v[:, 0]
+    d[200:300] = e1[200:300]                       # parallel to an edge of the plane
+    d[300:400] = (v[300:400, 0] - org[300:400])    # through vertex a
+    d[400:500] = (0.5 * (v[400:500, 1] + v[400:500, 2]) - org[400:500])   # through edge midpoint
+    d[500:550] = 0.0                               # zero direction
+    d[550:600] = -(v[550:600].mean(1) - org[550:600])   # pointing away (t < 0)
+    cases.append(np.concatenate([v.reshape(k, 9), org, d], 1))
+    # axis-aligned Cornell-like quads, rays from the camera
+    k = 400
+    cam = np.array([2.81432, 4.20749, -9.11751], np.float32)
+    a = np.zeros((k, 3), np.float32); b = np.zeros((k, 3), np.float32); c = np.zeros((k, 3), np.float32)
+    a[:, 0] = rng.uniform(0, 2, k); b[:, 0] = a[:, 0] + 3; c[:, 0] = a[:, 0]
+    a[:, 2] = rng.uniform(0, 2, k); b[:, 2] = a[:, 2]; c[:, 2] = a[:, 2] + 3
+    tgt = (a + b + c) / 3 + rng.normal(size=(k, 3)).astype(np.float32) * 0.8
+    tgt[:, 1] = 0
+    cases.append(np.concatenate([a, b, c, np.repeat(cam[None], k, 0), tgt - cam], 1))
+    cases = np.concatenate(cases).astype("<f4")
+    cases.tofile(tmp("mt.in"))
+    run("mt", tmp("mt.in"), tmp("mt.out"))
+    res = np.fromfile(tmp("mt.out"), np.dtype([("hit", "<i4"), ("t", "<f8")]))
+    np.savez_compressed(os.path.join(GOLDEN, "mt_cases.npz"), cases=cases, hit=res["hit"], t=res["t"])
+
+
+def gen_aabb(rng):
+    k = 4000
+    mn = rng.normal(size=(k, 3)).astype(np.float32)
+    ext = np.abs(rng.normal(size=(k, 3))).astype(np.float32)
+    ext[:500, rng.integers(0, 3)] = 0.0            # flat boxes (axis-aligned walls)
+    mx = mn + ext
+    o = (rng.normal(size=(k, 3)) * 3).astype(np.float32)
+    d = rng.normal(size=(k, 3)).astype(np.float32)
+    # signed zero and axis-aligned directions; origins on slab planes -> 0*inf = NaN
+    d[1000:1600, 0] = 0.0
+    d[1300:1600, 0] = -0.0
+    d[1600:2000, 1] = 0.0
+    d[1600:1800, 2] = -0.0
+    o[1000:1400, 0] = mn[1000:1400, 0]
+    o[1600:1700, 1] = mx[1600:1700, 1]
+    o[2000:2200] = (mn[2000:2200] + mx[2000:2200]) / 2      # inside
+    d[2200:2300] = 0.0                                      # zero direction
+    d[2300:2400] = np.float32(1e-30) * np.sign(d[2300:2400])  # tiny directions (huge reciprocals)
+    cases = np.concatenate([mn, mx, o, d], 1).astype("<f4")
+    cases.tofile(tmp("aabb.in"))
+    run("aabb", tmp("aabb.in"), tmp("aabb.out"))
+    hit = np.fromfile(tmp("aabb.out"), "<i4")
+    np.savez_compressed(os.path.join(GOLDEN, "aabb_cases.npz"), cases=cases, hit=hit)
+
+
+def gen_light(rng):
+    k = 3000
+    u = rng.integers(0, 2**32, (k, 3), dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0, 1, 0x7FFFFFFF, 0x80000000, 0xFFFFFF7F, 0xFFFFFF80, 0xFFFFFFFF], np.uint32)
+    u[:300] = rng.choice(edge, (300, 3))
+    u.astype("<u4").tofile(tmp("light.in"))
+    run("light", CORNELL_DIR, tmp("light.in"), tmp("light.out"))
+    res = np.fromfile(tmp("light.out"), np.dtype([("loc", "<f4", 3), ("n", "<f4", 3), ("emission", "<f4", 3), ("pdf", "<f4")]))
+    np.savez_compressed(os.path.join(GOLDEN, "light_cases.npz"), u=u, loc=res["loc"], n=res["n"], emission=res["emission"], pdf=res["pdf"])
+
+
+def gen_material(rng):
+    k = 3000
+    n = rng.normal(size=(k, 3)).astype(np.float32)
+    n /= np.linalg.norm(n, axis=1, keepdims=True)
+    axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1]], np.float32)
+    n[:300] = axes[rng.integers(0, 6, 300)]
+    n[300:400, 1] = n[300:400, 0]          # |n.x| == |n.y| tie
+    n = n.astype(np.float32)
+    wi = rng.normal(size=(k, 3)).astype(np.float32)
+    u = rng.integers(0, 2**32, (k, 2), dtype=np.uint64).astype(np.uint32)
+    edge = np.array([0, 1, 0x80000000, 0xFFFFFF7F, 0xFFFFFF80, 0xFFFFFFFF], np.uint32)
+    u[:200] = rng.choice(edge, (200, 2))
+    alb = rng.integers(0, 3, k).astype(np.uint32)
+    rec = np.concatenate([n.view(np.uint32), wi.view(np.uint32), u, alb[:, None]], 1).astype("<u4")
+    rec.tofile(tmp("mat.in"))
+    run("material", tmp("mat.in"), tmp("mat.out"))
+    res = np.fromfile(tmp("mat.out"), np.dtype([("raw", "<f4", 3), ("dir", "<f4", 3), ("brdf", "<f4", 3), ("pdf", "<f4")]))
+    np.savez_compressed(os.path.join(GOLDEN, "material_cases.npz"), n=n, wi=wi, u=u, albedo_index=alb,
+                        raw=res["raw"], dir=res["dir"], brdf=res["brdf"], pdf=res["pdf"])
+
+
+def gen_camera():
+    out = {}
+    for (W, H, frame, seed) in [(16, 16, 1, 0), (12, 9, 3, 42), (4, 4, 1, 7), (17, 13, 2, 0)]:
+        run("camera", W, H, frame, seed, tmp("cam"))
+        b = np.fromfile(tmp("cam"), np.uint8)
+        mats = b[:256].view("<f4").reshape(4, 4, 4)
+        vec = b[256:280].view("<f4")
+        inj = b[280:284].view("<i4")[0]
+        dirs = b[284:].view("<f4").reshape(-1, 3)
+        key = f"{W}x{H}_f{frame}_s{seed}"
+        out[f"mats_{key}"] = mats
+        out[f"dirs_{key}"] = dirs
+        out[f"vec_{key}"] = vec
+        assert inj == 1
+    for (W, H) in [(784, 784), (1920, 1080), (3840, 2160), (1280, 960), (640, 480), (64, 64), (128, 128), (40, 30)]:
+        run("camera", W, H, 1, 0, tmp("cam"))
+        b = np.fromfile(tmp("cam"), np.uint8)
+        out[f"mats_{W}x{H}"] = b[:256].view("<f4").reshape(4, 4, 4)
+    np.savez_compressed(os.path.join(GOLDEN, "camera.npz"), **out)
+
+
+def gen_images():
+    out = {}
+    for (W, H, spp, seed, rr) in [(64, 64, 1, 0, 0.8), (64, 64, 16, 0, 0.8), (64, 64, 256, 0, 0.8), (128, 128, 16, 7, 0.8),
+                                  (40, 30, 8, 123, 0.5), (33, 17, 4, 5, 0.9)]:
+        run("image", CORNELL_DIR, "", W, H, spp, seed, rr, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        key = f"{W}x{H}_spp{spp}_s{seed}_rr{rr}"
+        out[f"accum_{key}"] = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        out[f"rgba_{key}"] = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
+    np.savez_compressed(os.path.join(GOLDEN, "images_cornell.npz"), **out)
+
+
+def main():
+    global TMP
+    if not os.path.exists(HARNESS):
+        subprocess.check_call(["make", "-C", HERE, "ref"])
+    os.makedirs(GOLDEN, exist_ok=True)
+    rng = np.random.default_rng(20260101)
+    with tempfile.TemporaryDirectory() as TMP:
+        tris = gen_scene()
+        gen_rays(tris, rng)
+        gen_mt(rng)
+        gen_aabb(rng)
+        gen_light(rng)
+        gen_material(rng)
+        gen_camera()
+        gen_images()
+    print("golden fixtures written to", GOLDEN)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,83 @@
+/* oracle/rt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's Monte Carlo path-tracing hot path
+ * (IQ404/cpu-based-ray-tracer, "Monte Carlo Path Tracer" project; aliases as in SURVEY.md:
+ * MC/ = Monte Carlo Path Tracer/8599RayTracerGUI/src/, GLM/ = .../Walnut/vendor/glm/glm/).
+ * Used ONLY by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker.
+ * The product (cpu-based-ray-tracer_amd/) never links or calls it.
+ *
+ * Pinning: every sub-function is checked bit-exactly against golden vectors produced by
+ * oracle/_ref/ref_harness (the reference's own BVH/triangle/material/camera code compiled from
+ * /root/reference), and whole images against the harness's hybrid renders
+ * (tests/golden/, generator oracle/gen_golden.py).
+ */
+#ifndef RT_ORACLE_H
+#define RT_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_scene or_scene;
+
+/* per-sample work counters (summed) */
+typedef struct {
+    uint64_t samples, rays, node_tests, tri_tests, draws, shading_calls, max_depth;
+} or_counters;
+
+/* objl::Loader::LoadFile subset (MC/OBJ_Loader.h:434-720): de-indexed vertex positions of the
+ * first mesh.  Returns the number of floats written (3 per vertex) or -1; out may be NULL to query. */
+int64_t or_obj_positions(const char* path, float* out, int64_t cap_floats);
+
+or_scene* or_scene_new(void);
+/* one TriangleMesh (MC/TriangleMesh.h:148-186): raw objl positions (pre-scale, 9 floats per
+ * triangle), scale 0.01f applied inside; albedo = diffuse_coefficient, emission per
+ * WhittedMaterial (MC/WhittedMaterial.h:24-42). Returns mesh index. */
+int or_scene_add_mesh(or_scene* s, const float* raw_positions, int64_t n_tris, const float albedo[3], const float emission[3]);
+/* Renderer::GenerateBVH (MC/Renderer.h:83-86): top-level BVH over the meshes. */
+int or_scene_build(or_scene* s);
+void or_scene_free(or_scene* s);
+int or_scene_num_tris(const or_scene* s);
+int or_scene_num_nodes(const or_scene* s);
+/* flattened DFS pre-order dump (same record meaning as the ref harness `scene` command):
+ * node: min[3] max[3] area left right tri mesh top ; tri: a b c n area mesh material */
+int or_scene_dump(const or_scene* s, float* node_f /*7 per node*/, int32_t* node_i /*5 per node*/,
+                  float* tri_f /*13 per tri*/, int32_t* tri_i /*2 per tri*/);
+
+/* closest hit of n rays (BVH::traverse_BVH_from_root, MC/BVH.h:72-101): hit, flattened tri id,
+ * material id, double t, location, normal */
+void or_trace(const or_scene* s, int64_t n, const float* org, const float* dir,
+              int32_t* hit, int32_t* tri, int32_t* mat, double* t, float* loc, float* nrm);
+
+/* Whitted::RayTriangleIntersection (MC/TriangleMesh.h:19-45); 15 floats per case */
+void or_mt(int64_t n, const float* cases, int32_t* hit, double* t);
+/* AABB_3D::intersects_with_ray (MC/BoundingVolume.h:173-215); 12 floats per case */
+void or_aabb(int64_t n, const float* cases, int32_t* hit);
+
+/* Camera (MC/Camera.cpp:87-132) with the defaults of MC/Camera.h:19-37, fov 35 (MC/mainloop.cpp:22):
+ * mats = proj, invProj, view, invView (column-major, 16 floats each) */
+void or_camera_matrices(uint32_t W, uint32_t H, float mats[64]);
+/* jittered direction of pixel (x,y) at `frame` (before RayGen's re-normalisation) */
+void or_camera_dirs(uint32_t W, uint32_t H, uint32_t frame, uint64_t seed, float* dirs /* W*H*3 */);
+
+/* Renderer::Render x spp (MC/Renderer.cpp:91-134): frames first_frame .. first_frame+n_frames-1
+ * accumulated into accum (float4 per pixel, caller-initialised), final RGBA8 (ABGR u32) written to
+ * rgba.  Rows [row_begin,row_end) only (row_end = 0 means H).  threads <= 0: hardware threads. */
+int or_render(const or_scene* s, uint32_t W, uint32_t H, uint32_t first_frame, uint32_t n_frames, uint64_t seed,
+              float rr, int threads, uint32_t row_begin, uint32_t row_end,
+              float* accum, uint32_t* rgba, or_counters* counters);
+
+/* unit entry points with explicit u32 draws: SamplingAreaLight (3 draws per case) and
+ * WhittedMaterial::Sampling + normalize + BRDF + PDF (2 draws per case) */
+void or_light_sample(const or_scene* s, int64_t n, const uint32_t* u, float* loc, float* nrm, float* emission, float* pdf);
+void or_material_sample(int64_t n, const float* nrm, const float* wi, const uint32_t* u, const float* albedo,
+                        float* raw, float* dir, float* brdf, float* pdf);
+
+/* the RNG stream itself (oracle/philox.h) */
+uint32_t or_rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim);
+float or_rng_float(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
