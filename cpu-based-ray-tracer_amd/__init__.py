@@ -1,0 +1,255 @@
+"""cpu-based-ray-tracer_amd -- MI355X-native Monte Carlo path tracer (host binding).
+
+Thin ctypes binding of the C-ABI in include/rt_capi.h (librt_hip.so, built in-tree by `make`).
+The product path is the HIP megakernel; there is no CPU fallback: if the shared library is
+missing or a call fails, an exception is raised.
+
+Load it by path (the directory name is not a Python identifier):
+    import importlib.util, os
+    spec = importlib.util.spec_from_file_location("rt_amd", "cpu-based-ray-tracer_amd/__init__.py")
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+
+RT_OK = 0
+RENDER_EXACT = 1
+RENDER_COUNT = 2
+
+_lib = None
+
+
+class RtError(RuntimeError):
+    pass
+
+
+class Camera(C.Structure):
+    _fields_ = [("position", C.c_float * 3), ("inv_projection", C.c_float * 16), ("inv_view", C.c_float * 16)]
+
+
+class DeviceCfg(C.Structure):
+    _fields_ = [("device", C.c_int32), ("stream", C.c_void_p), ("flags", C.c_uint32)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("first_frame", C.c_uint32), ("n_frames", C.c_uint32), ("seed", C.c_uint64), ("rr", C.c_float), ("flags", C.c_uint32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("last_kernel_ms", C.c_float), ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("rays", C.c_uint64),
+                ("stack_overflows", C.c_uint64), ("samples", C.c_uint64), ("grid", C.c_uint32), ("block", C.c_uint32),
+                ("stack_depth", C.c_uint32)]
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("n_meshes", C.c_uint32), ("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_light_tris", C.c_uint32),
+                ("max_depth", C.c_uint32), ("light_mesh", C.c_int32), ("light_area", C.c_float), ("device_bytes", C.c_uint64)]
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def lib():
+    """Load librt_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RtError(f"{LIB_PATH} not built: run `make -C {PKG_DIR}` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32, fp = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32, C.POINTER(C.c_float)
+    sig = {
+        "rt_api_version": (i32, []),
+        "rt_scene_create": (i32, [C.POINTER(vp)]),
+        "rt_scene_destroy": (None, [vp]),
+        "rt_scene_add_cornell_box": (i32, [vp]),
+        "rt_scene_add_obj": (i32, [vp, C.c_char_p, fp, fp, C.POINTER(i32)]),
+        "rt_scene_add_mesh": (i32, [vp, fp, u64, fp, fp, C.POINTER(i32)]),
+        "rt_scene_build": (i32, [vp]),
+        "rt_scene_get_info": (i32, [vp, C.POINTER(SceneInfo)]),
+        "rt_scene_export": (i32, [vp, fp, C.POINTER(i32), fp, C.POINTER(i32)]),
+        "rt_camera_default": (i32, [u32, u32, C.POINTER(Camera), fp, fp]),
+        "rt_camera_look": (i32, [u32, u32, fp, fp, C.c_float, C.c_float, C.c_float, C.POINTER(Camera)]),
+        "rt_create": (i32, [C.POINTER(vp), C.POINTER(DeviceCfg)]),
+        "rt_destroy": (None, [vp]),
+        "rt_last_error": (C.c_char_p, [vp]),
+        "rt_upload_scene": (i32, [vp, vp]),
+        "rt_resize": (i32, [vp, u32, u32, u32, u32, u32]),
+        "rt_local_rows": (u32, [vp]),
+        "rt_render": (i32, [vp, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(u32), fp]),
+        "rt_device_buffers": (i32, [vp, C.POINTER(vp), C.POINTER(vp)]),
+        "rt_copy_rgba_to_device": (i32, [vp, vp]),
+        "rt_reset_accumulation": (i32, [vp]),
+        "rt_synchronize": (i32, [vp]),
+        "rt_get_stats": (i32, [vp, C.POINTER(Stats)]),
+        "rt_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(C.c_double)]),
+        "rt_math_selftest": (i32, [vp, u64, fp, fp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+
+class Scene:
+    """Host scene: meshes + reference-identical BVH build (rt_scene_*)."""
+
+    def __init__(self):
+        self.h = C.c_void_p()
+        self._check(lib().rt_scene_create(C.byref(self.h)), "rt_scene_create")
+
+    @staticmethod
+    def _check(st, what):
+        if st != RT_OK:
+            raise RtError(f"{what} failed with status {st}")
+
+    @classmethod
+    def cornell(cls, extra=()):
+        s = cls()
+        s._check(lib().rt_scene_add_cornell_box(s.h), "rt_scene_add_cornell_box")
+        for (raw, albedo, emission) in extra:
+            s.add_mesh(raw, albedo, emission)
+        s.build()
+        return s
+
+    def add_mesh(self, raw, albedo, emission):
+        raw = np.ascontiguousarray(raw, np.float32).reshape(-1, 9)
+        mid = C.c_int32()
+        self._check(lib().rt_scene_add_mesh(self.h, _fp(raw), raw.shape[0], _fp(np.asarray(albedo, np.float32)),
+                                            _fp(np.asarray(emission, np.float32)), C.byref(mid)), "rt_scene_add_mesh")
+        return mid.value
+
+    def add_obj(self, path, albedo, emission):
+        mid = C.c_int32()
+        self._check(lib().rt_scene_add_obj(self.h, path.encode(), _fp(np.asarray(albedo, np.float32)),
+                                           _fp(np.asarray(emission, np.float32)), C.byref(mid)), "rt_scene_add_obj")
+        return mid.value
+
+    def build(self):
+        self._check(lib().rt_scene_build(self.h), "rt_scene_build")
+        return self
+
+    def info(self):
+        i = SceneInfo()
+        self._check(lib().rt_scene_get_info(self.h, C.byref(i)), "rt_scene_get_info")
+        return i
+
+    def export(self):
+        i = self.info()
+        nf = np.zeros((i.n_nodes, 7), np.float32); ni = np.zeros((i.n_nodes, 5), np.int32)
+        tf = np.zeros((i.n_tris, 13), np.float32); ti = np.zeros((i.n_tris, 2), np.int32)
+        self._check(lib().rt_scene_export(self.h, _fp(nf), ni.ctypes.data_as(C.POINTER(C.c_int32)), _fp(tf),
+                                          ti.ctypes.data_as(C.POINTER(C.c_int32))), "rt_scene_export")
+        return nf, ni, tf, ti
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().rt_scene_destroy(self.h)
+                self.h = C.c_void_p()
+        except Exception:
+            pass
+
+
+def camera_default(W, H):
+    cam = Camera()
+    proj = np.zeros(16, np.float32); view = np.zeros(16, np.float32)
+    st = lib().rt_camera_default(W, H, C.byref(cam), _fp(proj), _fp(view))
+    if st != RT_OK:
+        raise RtError(f"rt_camera_default failed {st}")
+    return cam, proj, view
+
+
+class Context:
+    """One GPU: device buffers, stream, megakernel launches (rt_create .. rt_destroy)."""
+
+    def __init__(self, device=0, stream=None):
+        self.h = C.c_void_p()
+        cfg = DeviceCfg(device, C.c_void_p(stream) if stream else None, 0)
+        st = lib().rt_create(C.byref(self.h), C.byref(cfg))
+        if st != RT_OK:
+            raise RtError(f"rt_create failed with status {st} (is a GPU visible?)")
+        self.W = self.H = 0
+        self.local_rows = 0
+
+    def _check(self, st, what):
+        if st != RT_OK:
+            msg = lib().rt_last_error(self.h)
+            raise RtError(f"{what} failed ({st}): {msg.decode() if msg else ''}")
+
+    def upload(self, scene):
+        self._check(lib().rt_upload_scene(self.h, scene.h), "rt_upload_scene")
+
+    def resize(self, W, H, band=8, rank=0, nranks=1):
+        self._check(lib().rt_resize(self.h, W, H, band, rank, nranks), "rt_resize")
+        self.W, self.H = W, H
+        self.band, self.rank, self.nranks = band, rank, nranks
+        self.local_rows = lib().rt_local_rows(self.h)
+
+    def render(self, cam, n_frames, first_frame=1, seed=0, rr=0.8, exact=True, count=False, fetch=True):
+        p = RenderParams(first_frame, n_frames, seed, rr, (RENDER_EXACT if exact else 0) | (RENDER_COUNT if count else 0))
+        if fetch:
+            rgba = np.zeros((self.local_rows, self.W), np.uint32)
+            acc = np.zeros((self.local_rows, self.W, 4), np.float32)
+            self._check(lib().rt_render(self.h, C.byref(cam), C.byref(p), rgba.ctypes.data_as(C.POINTER(C.c_uint32)), _fp(acc)), "rt_render")
+            return rgba, acc
+        self._check(lib().rt_render(self.h, C.byref(cam), C.byref(p), None, None), "rt_render")
+        return None
+
+    def stats(self):
+        s = Stats()
+        self._check(lib().rt_get_stats(self.h, C.byref(s)), "rt_get_stats")
+        return s
+
+    def sync(self):
+        self._check(lib().rt_synchronize(self.h), "rt_synchronize")
+
+    def device_buffers(self):
+        a, r = C.c_void_p(), C.c_void_p()
+        self._check(lib().rt_device_buffers(self.h, C.byref(a), C.byref(r)), "rt_device_buffers")
+        return a.value, r.value
+
+    def copy_rgba_to_device(self, dst_ptr):
+        self._check(lib().rt_copy_rgba_to_device(self.h, C.c_void_p(dst_ptr)), "rt_copy_rgba_to_device")
+
+    def trace(self, org, dirs):
+        org = np.ascontiguousarray(org, np.float32); dirs = np.ascontiguousarray(dirs, np.float32)
+        n = org.shape[0]
+        tri = np.zeros(n, np.int32); t = np.zeros(n, np.float64)
+        self._check(lib().rt_trace(self.h, n, _fp(org), _fp(dirs), tri.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   t.ctypes.data_as(C.POINTER(C.c_double))), "rt_trace")
+        return tri, t
+
+    def math_selftest(self, x):
+        x = np.ascontiguousarray(x, np.float32)
+        out = np.zeros((x.shape[0], 6), np.float32)
+        self._check(lib().rt_math_selftest(self.h, x.shape[0], _fp(x), _fp(out)), "rt_math_selftest")
+        return out
+
+    def local_to_global_rows(self):
+        """global row index of every local row (row bands dealt round-robin)."""
+        rows = []
+        b = self.rank
+        while b * self.band < self.H:
+            rows.extend(range(b * self.band, min((b + 1) * self.band, self.H)))
+            b += self.nranks
+        return np.array(rows, np.int64)
+
+    def close(self):
+        if self.h:
+            lib().rt_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,418 @@
+// rt_capi.cpp -- implementation of include/rt_capi.h (host side; compiled by hipcc, links the HIP runtime).
+#include "rt_capi.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "rt_kernels.h"
+#include "rt_scene.h"
+
+struct rt_scene {
+    rt::SceneBuilder builder;
+    rt::FlatScene flat;
+    bool built = false;
+};
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    // scene
+    float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr;
+    rt_scene_header hdr{};
+    bool has_scene = false;
+    // image
+    uint32_t W = 0, H = 0, band = 8, rank = 0, nranks = 1, local_rows = 0;
+    float4* d_accum = nullptr;
+    uint32_t* d_rgba = nullptr;
+    // scratch
+    uint32_t* d_counter = nullptr;
+    unsigned long long* d_counters = nullptr;
+    float4* d_stack_ld = nullptr;
+    int32_t* d_stack_mat = nullptr;
+    uint32_t stack_depth = 0;
+    uint32_t grid = 0, block = 256, total_threads = 0;   // grid of the EXACT kernel (sizes the fold stack)
+    uint32_t n_cu = 0;
+    int occ[2][2] = {{0, 0}, {0, 0}};                     // blocks per CU, [exact][count]
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    rt_stats stats{};
+    bool pending_stats = false;
+    uint32_t last_flags = 0;
+};
+
+namespace {
+
+constexpr uint32_t kStackDepth = 192;   // EXACT fold stack; RR 0.8 => P(depth > 192) ~ 2.5e-19 per sample
+
+rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what)
+{
+    if (c) c->err = std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")";
+    return e == hipErrorOutOfMemory ? RT_ERR_OOM : RT_ERR_HIP;
+}
+#define HIPC(ctx, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_fail(ctx, e_, #call); \
+    } while (0)
+
+template <class T> void dfree(T*& p) { if (p) { (void)hipFree((void*)p); p = nullptr; } }
+
+template <class T> rt_status upload(rt_ctx* c, T*& dst, const std::vector<float>& src)
+{
+    dfree(dst);
+    if (src.empty()) return RT_OK;
+    HIPC(c, hipMalloc((void**)&dst, src.size() * sizeof(float)));
+    HIPC(c, hipMemcpy((void*)dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+uint32_t count_local_rows(uint32_t H, uint32_t band, uint32_t rank, uint32_t nranks)
+{
+    uint32_t n = 0;
+    for (uint32_t b = rank; b * band < H; b += nranks) n += std::min(band, H - b * band);
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rt_api_version(void) { return RT_API_VERSION; }
+
+// ------------------------------------------------------------------ scene
+rt_status rt_scene_create(rt_scene** out)
+{
+    if (!out) return RT_ERR_INVALID;
+    *out = new (std::nothrow) rt_scene;
+    return *out ? RT_OK : RT_ERR_OOM;
+}
+void rt_scene_destroy(rt_scene* s) { delete s; }
+
+rt_status rt_scene_add_cornell_box(rt_scene* s)
+{
+    if (!s) return RT_ERR_INVALID;
+    s->builder.add_cornell_box();
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_mesh(rt_scene* s, const float* raw, uint64_t n_tris, const float albedo[3], const float emission[3], int32_t* mesh_id)
+{
+    if (!s || (!raw && n_tris) || !albedo || !emission || n_tris == 0) return RT_ERR_INVALID;
+    rt::MeshDesc m;
+    m.raw.assign(raw, raw + 9 * n_tris);
+    m.material = rt::MaterialDesc{{albedo[0], albedo[1], albedo[2]}, {emission[0], emission[1], emission[2]}};
+    m.name = "mesh" + std::to_string(s->builder.num_meshes());
+    const int id = s->builder.add_mesh(std::move(m));
+    if (mesh_id) *mesh_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_obj(rt_scene* s, const char* path, const float albedo[3], const float emission[3], int32_t* mesh_id)
+{
+    if (!s || !path || !albedo || !emission) return RT_ERR_INVALID;
+    rt::MeshDesc m;
+    std::string err;
+    if (!rt::SceneBuilder::load_obj_positions(path, m.raw, err) || m.raw.empty()) return RT_ERR_IO;
+    m.material = rt::MaterialDesc{{albedo[0], albedo[1], albedo[2]}, {emission[0], emission[1], emission[2]}};
+    m.name = path;
+    const int id = s->builder.add_mesh(std::move(m));
+    if (mesh_id) *mesh_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_build(rt_scene* s)
+{
+    if (!s) return RT_ERR_INVALID;
+    std::string err;
+    if (!s->builder.build(s->flat, err)) return RT_ERR_INVALID;
+    s->built = true;
+    return RT_OK;
+}
+
+rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
+{
+    if (!s || !info || !s->built) return s && !s->built ? RT_ERR_STATE : RT_ERR_INVALID;
+    const auto& h = s->flat.hdr;
+    info->n_meshes = h.n_mats;
+    info->n_tris = h.n_tris;
+    info->n_nodes = h.n_nodes;
+    info->n_light_tris = h.n_ltris;
+    info->max_depth = h.max_depth;
+    info->light_mesh = h.light_mesh;
+    info->light_area = h.light_area;
+    info->device_bytes = (s->flat.nodes.size() + s->flat.tris.size() + s->flat.mats.size() + s->flat.lnodes.size() + s->flat.ltris.size()) * 4;
+    return RT_OK;
+}
+
+rt_status rt_scene_export(const rt_scene* s, float* nf, int32_t* ni, float* tf, int32_t* ti)
+{
+    if (!s || !s->built) return RT_ERR_STATE;
+    const auto& f = s->flat;
+    if (nf) std::memcpy(nf, f.dbg_node_f.data(), f.dbg_node_f.size() * 4);
+    if (ni) std::memcpy(ni, f.dbg_node_i.data(), f.dbg_node_i.size() * 4);
+    if (tf) std::memcpy(tf, f.dbg_tri_f.data(), f.dbg_tri_f.size() * 4);
+    if (ti) std::memcpy(ti, f.dbg_tri_i.data(), f.dbg_tri_i.size() * 4);
+    return RT_OK;
+}
+
+// ------------------------------------------------------------------ context
+rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
+{
+    if (!out) return RT_ERR_INVALID;
+    *out = nullptr;
+    rt_ctx* c = new (std::nothrow) rt_ctx;
+    if (!c) return RT_ERR_OOM;
+    c->device = cfg ? cfg->device : 0;
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
+    if (cfg && cfg->stream) {
+        c->stream = (hipStream_t)cfg->stream;
+    } else {
+        e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipStreamCreate"); delete c; return s; }
+        c->own_stream = true;
+    }
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 64) != hipSuccess) {
+        c->err = "context allocation failed";
+        rt_destroy(c);
+        return RT_ERR_HIP;
+    }
+    // persistent grid: every CU filled to the kernel's occupancy
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) { c->err = "hipGetDeviceProperties failed"; rt_destroy(c); return RT_ERR_HIP; }
+    // all instantiations are sized by the most register-hungry one so one stack serves every mode;
+    // the occupancy query is advisory only: the kernel has no grid barrier, a non-resident block
+    // simply starts later and finds the queue drained
+    c->n_cu = (uint32_t)prop.multiProcessorCount;
+    int ex_max = 1;
+    for (int ex = 0; ex < 2; ++ex)
+        for (int cn = 0; cn < 2; ++cn) {
+            int b = rt_megakernel_occupancy(ex, cn, 256);
+            c->occ[ex][cn] = b > 0 ? b : 2;
+            if (ex) ex_max = std::max(ex_max, c->occ[ex][cn]);
+        }
+    c->block = 256;
+    c->grid = c->n_cu * (uint32_t)ex_max;
+    c->total_threads = c->grid * c->block;
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris);
+    dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
+{
+    if (!c || !s) return RT_ERR_INVALID;
+    if (!s->built) { c->err = "scene not built (rt_scene_build)"; return RT_ERR_STATE; }
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    rt_status r;
+    if ((r = upload(c, c->d_nodes, s->flat.nodes)) != RT_OK) return r;
+    if ((r = upload(c, c->d_tris, s->flat.tris)) != RT_OK) return r;
+    if ((r = upload(c, c->d_mats, s->flat.mats)) != RT_OK) return r;
+    if ((r = upload(c, c->d_lnodes, s->flat.lnodes)) != RT_OK) return r;
+    if ((r = upload(c, c->d_ltris, s->flat.ltris)) != RT_OK) return r;
+    c->hdr = s->flat.hdr;
+    c->has_scene = true;
+    return RT_OK;
+}
+
+rt_status rt_resize(rt_ctx* c, uint32_t W, uint32_t H, uint32_t band, uint32_t rank, uint32_t nranks)
+{
+    if (!c || W == 0 || H == 0 || band == 0 || nranks == 0 || rank >= nranks) return RT_ERR_INVALID;
+    if (W > 65536 || H > 65536) { c->err = "viewport too large"; return RT_ERR_INVALID; }
+    HIPC(c, hipSetDevice(c->device));
+    const uint32_t rows = count_local_rows(H, band, rank, nranks);
+    if (W == c->W && H == c->H && band == c->band && rank == c->rank && nranks == c->nranks && c->d_accum) return RT_OK;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_accum); dfree(c->d_rgba);
+    c->W = W; c->H = H; c->band = band; c->rank = rank; c->nranks = nranks; c->local_rows = rows;
+    const size_t npx = (size_t)std::max<uint32_t>(rows, 1) * W;
+    HIPC(c, hipMalloc((void**)&c->d_accum, npx * sizeof(float4)));
+    HIPC(c, hipMalloc((void**)&c->d_rgba, npx * sizeof(uint32_t)));
+    HIPC(c, hipMemsetAsync(c->d_accum, 0, npx * sizeof(float4), c->stream));
+    HIPC(c, hipMemsetAsync(c->d_rgba, 0, npx * sizeof(uint32_t), c->stream));
+    return RT_OK;
+}
+
+uint32_t rt_local_rows(const rt_ctx* c) { return c ? c->local_rows : 0; }
+
+rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, uint32_t* out_rgba, float* out_accum)
+{
+    if (!c || !cam || !p) return RT_ERR_INVALID;
+    if (!c->has_scene) { c->err = "no scene uploaded"; return RT_ERR_STATE; }
+    if (!c->d_accum) { c->err = "no viewport (rt_resize)"; return RT_ERR_STATE; }
+    if (p->first_frame == 0) { c->err = "first_frame is 1-based"; return RT_ERR_INVALID; }
+    // a survival probability >= 1 never terminates a path in a closed scene (the reference recurses
+    // until its stack overflows); reject it, and NaN
+    if (!(p->rr >= 0.0f && p->rr < 1.0f)) { c->err = "rr must be in [0, 1)"; return RT_ERR_INVALID; }
+    HIPC(c, hipSetDevice(c->device));
+    const bool exact = (p->flags & RT_RENDER_EXACT) != 0, count = (p->flags & RT_RENDER_COUNT) != 0;
+    if (exact && !c->d_stack_ld) {
+        c->stack_depth = kStackDepth;
+        HIPC(c, hipMalloc((void**)&c->d_stack_ld, (size_t)c->stack_depth * c->total_threads * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_stack_mat, (size_t)c->stack_depth * c->total_threads * sizeof(int32_t)));
+    }
+    KParams P{};
+    P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes;
+    P.tris = c->d_tris; P.mats = c->d_mats; P.lnodes = c->d_lnodes; P.ltris = c->d_ltris;
+    P.light_area = c->hdr.light_area;
+    std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
+    P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;
+    std::memcpy(P.cam_pos, cam->position, sizeof P.cam_pos);
+    std::memcpy(P.iproj, cam->inv_projection, sizeof P.iproj);
+    std::memcpy(P.iview, cam->inv_view, sizeof P.iview);
+    P.W = c->W; P.H = c->H;
+    P.first_frame = p->first_frame; P.n_frames = p->n_frames;
+    P.seed = p->seed; P.rr = p->rr;
+    P.band = c->band; P.rank = c->rank; P.nranks = c->nranks; P.n_local_rows = c->local_rows;
+    P.tiles_x = (c->W + 7) / 8;
+    const uint64_t items = (uint64_t)((c->local_rows + 7) / 8) * P.tiles_x * 64;
+    if (items >= 0xFFFFFFFFull) { c->err = "image too large for one launch"; return RT_ERR_INVALID; }
+    P.n_items = (uint32_t)items;
+    P.accum = c->d_accum; P.rgba = c->d_rgba;
+    P.work_counter = c->d_counter;
+    P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
+    P.total_threads = c->total_threads;
+    P.counters = c->d_counters;
+    const uint32_t grid = exact ? c->grid : c->n_cu * (uint32_t)c->occ[0][count ? 1 : 0];
+    HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 64, c->stream));
+    c->last_flags = p->flags;
+    if (p->n_frames > 0 && c->local_rows > 0) {
+        HIPC(c, hipEventRecord(c->ev0, c->stream));
+        HIPC(c, rt_launch_megakernel(P, exact, count, grid, c->block, c->stream));
+        c->stats.grid = grid;
+        HIPC(c, hipEventRecord(c->ev1, c->stream));
+        c->pending_stats = true;
+    }
+    c->stats.samples = (uint64_t)c->local_rows * c->W * p->n_frames;
+    if (out_rgba || out_accum) {
+        const size_t npx = (size_t)c->local_rows * c->W;
+        if (out_rgba) HIPC(c, hipMemcpyAsync(out_rgba, c->d_rgba, npx * 4, hipMemcpyDeviceToHost, c->stream));
+        if (out_accum) HIPC(c, hipMemcpyAsync(out_accum, c->d_accum, npx * 16, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+    }
+    return RT_OK;
+}
+
+rt_status rt_device_buffers(rt_ctx* c, void** d_accum, void** d_rgba)
+{
+    if (!c) return RT_ERR_INVALID;
+    if (d_accum) *d_accum = c->d_accum;
+    if (d_rgba) *d_rgba = c->d_rgba;
+    return RT_OK;
+}
+
+rt_status rt_copy_rgba_to_device(rt_ctx* c, void* dst)
+{
+    if (!c || !dst) return RT_ERR_INVALID;
+    HIPC(c, hipMemcpyAsync(dst, c->d_rgba, (size_t)c->local_rows * c->W * 4, hipMemcpyDeviceToDevice, c->stream));
+    return RT_OK;
+}
+
+rt_status rt_reset_accumulation(rt_ctx* c)
+{
+    if (!c || !c->d_accum) return RT_ERR_STATE;
+    HIPC(c, hipMemsetAsync(c->d_accum, 0, (size_t)std::max<uint32_t>(c->local_rows, 1) * c->W * sizeof(float4), c->stream));
+    return RT_OK;
+}
+
+rt_status rt_synchronize(rt_ctx* c)
+{
+    if (!c) return RT_ERR_INVALID;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
+{
+    if (!c || !st) return RT_ERR_INVALID;
+    if (c->pending_stats) {
+        HIPC(c, hipEventSynchronize(c->ev1));
+        float ms = 0.0f;
+        HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->stats.last_kernel_ms = ms;
+        unsigned long long h[4] = {0, 0, 0, 0};
+        HIPC(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+        c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[3];
+        c->pending_stats = false;
+    }
+    c->stats.block = c->block; c->stats.stack_depth = c->stack_depth;
+    *st = c->stats;
+    return RT_OK;
+}
+
+rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t)
+{
+    if (!c || (n && (!org || !dir || !tri || !t))) return RT_ERR_INVALID;
+    if (!c->has_scene) { c->err = "no scene uploaded"; return RT_ERR_STATE; }
+    if (n == 0) return RT_OK;
+    if (n > 0x7FFFFFFFull) return RT_ERR_INVALID;
+    HIPC(c, hipSetDevice(c->device));
+    float *d_o = nullptr, *d_d = nullptr; int32_t* d_tri = nullptr; double* d_t = nullptr;
+    auto cleanup = [&]() { dfree(d_o); dfree(d_d); dfree(d_tri); dfree(d_t); };
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_o, n * 12)) != hipSuccess || (e = hipMalloc((void**)&d_d, n * 12)) != hipSuccess ||
+        (e = hipMalloc((void**)&d_tri, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_t, n * 8)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "hipMalloc(rt_trace)");
+    }
+    KParams P{};
+    P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes; P.tris = c->d_tris;
+    if ((e = hipMemcpyAsync(d_o, org, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = rt_launch_trace(P, (uint32_t)n, d_o, d_d, d_tri, d_t, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(tri, d_tri, n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(t, d_t, n * 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_trace");
+    }
+    cleanup();
+    return RT_OK;
+}
+
+rt_status rt_math_selftest(rt_ctx* c, uint64_t n, const float* x, float* out)
+{
+    if (!c || (n && (!x || !out))) return RT_ERR_INVALID;
+    if (n == 0) return RT_OK;
+    HIPC(c, hipSetDevice(c->device));
+    float *d_x = nullptr, *d_out = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_x, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 24)) != hipSuccess) {
+        dfree(d_x); dfree(d_out); return hip_fail(c, e, "hipMalloc(selftest)");
+    }
+    if ((e = hipMemcpyAsync(d_x, x, n * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = rt_launch_math((uint32_t)n, d_x, d_out, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, d_out, n * 24, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        dfree(d_x); dfree(d_out); return hip_fail(c, e, "rt_math_selftest");
+    }
+    dfree(d_x); dfree(d_out);
+    return RT_OK;
+}
+
+}  // extern "C"

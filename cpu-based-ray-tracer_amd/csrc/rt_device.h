@@ -1,0 +1,157 @@
+// rt_device.h -- device arithmetic of the path tracer, in the reference's operation order.
+//
+// Every expression mirrors the reference (MC/ = "Monte Carlo Path Tracer/8599RayTracerGUI/src/")
+// and glm 0.9.9.9 (GLM/ = ".../Walnut/vendor/glm/glm/") term by term.  The file is compiled with
+// -ffp-contract=off, without fast-math, and with correctly rounded f32 division/sqrt, so each
+// operation is the same IEEE operation the CPU reference performs.  Transcendentals (cos/sin of the
+// hemisphere angle) are evaluated in double and rounded once (correctly rounded f32 results);
+// glibc's cosf/sinf differ from that in ~0.05-0.1 % of arguments by one ulp ("Parity").
+#ifndef RT_DEVICE_H
+#define RT_DEVICE_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+struct V3 { float x, y, z; };
+
+__device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 muls(V3 a, float s) { return V3{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V3 smul(float s, V3 a) { return V3{s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ V3 divs(V3 a, float s) { return V3{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ V3 neg(V3 a) { return V3{-a.x, -a.y, -a.z}; }
+// glm::dot, GLM/detail/func_geometric.inl:48-55
+__device__ __forceinline__ float dot(V3 a, V3 b) { float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return (tx + ty) + tz; }
+// glm::cross, GLM/detail/func_geometric.inl:68-80
+__device__ __forceinline__ V3 cross(V3 x, V3 y) { return V3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+// glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
+__device__ __forceinline__ V3 glm_normalize(V3 v) { float is = 1.0f / __builtin_sqrtf(dot(v, v)); return muls(v, is); }
+__device__ __forceinline__ float glm_length(V3 v) { return __builtin_sqrtf(dot(v, v)); }
+// Whitted::normalize (zero-safe), MC/VectorFloat.h:22-31
+__device__ __forceinline__ V3 w_normalize(V3 v)
+{
+    float l2 = ((v.x * v.x) + (v.y * v.y)) + (v.z * v.z);
+    if (l2 > 0.0f) { float inv = 1.0f / __builtin_sqrtf(l2); return V3{v.x * inv, v.y * inv, v.z * inv}; }
+    return v;
+}
+// std::max / std::min / glm::max / glm::min: compare-select, the first operand survives a NaN
+// (MC/BoundingVolume.h:207-208); never lowered to v_max_f32 (no nnan flag without fast-math)
+__device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
+__device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
+
+__device__ __forceinline__ int f2i(float f) { return __float_as_int(f); }
+
+constexpr float PI_F = 3.141592653589793f;            // MC/WhittedUtilities.h:20
+constexpr float INTERSECTION_CORRECTION = 0.00001f;   // MC/WhittedUtilities.h:18
+
+// ------------------------------------------------------------------------------ RNG
+// Frozen stream (oracle/philox.h restates it independently): Philox4x32-10, key = seed,
+// counter = (pixel, frame, dim >> 2, 0), u32 = out[dim & 3], Float = (float)u / (float)UINT32_MAX
+// (Walnut::Random::Float, WN/Random.h:27-30).
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4])
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+struct Rng {
+    uint32_t k0, k1, pixel, frame, dim;
+    uint32_t blk;
+    uint32_t b0, b1, b2, b3;
+    __device__ __forceinline__ void start(uint64_t seed, uint32_t px, uint32_t fr)
+    {
+        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); pixel = px; frame = fr; dim = 0; blk = 0xFFFFFFFFu;
+    }
+    __device__ __forceinline__ float next()
+    {
+        const uint32_t want = dim >> 2;
+        if (want != blk) {
+            uint32_t o[4];
+            philox4x32_10(pixel, frame, want, 0u, k0, k1, o);
+            b0 = o[0]; b1 = o[1]; b2 = o[2]; b3 = o[3];
+            blk = want;
+        }
+        const uint32_t s = dim & 3u;
+        const uint32_t u = s == 0 ? b0 : (s == 1 ? b1 : (s == 2 ? b2 : b3));
+        ++dim;
+        return (float)u / 4294967296.0f;   // (float)UINT32_MAX == 2^32 exactly
+    }
+};
+
+// ------------------------------------------------------------------------------ ray / slab / MT
+struct Ray {   // AccelerationStructure::Ray, MC/Ray.h:23-44
+    V3 o, d, rcp;
+    bool nx, ny, nz;
+};
+__device__ __forceinline__ Ray make_ray(V3 o, V3 d)
+{
+    Ray r;
+    r.o = o; r.d = d;
+    r.rcp = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    r.nx = d.x < 0.0f; r.ny = d.y < 0.0f; r.nz = d.z < 0.0f;
+    return r;
+}
+
+// AABB_3D::intersects_with_ray, MC/BoundingVolume.h:173-215.  Selecting the far slab for a
+// negative direction before the subtraction yields exactly the swapped values.
+__device__ __forceinline__ bool slab_hit(const Ray& r, float lx, float ly, float lz, float hx, float hy, float hz)
+{
+    const float ax = r.nx ? hx : lx, bx = r.nx ? lx : hx;
+    const float ay = r.ny ? hy : ly, by = r.ny ? ly : hy;
+    const float az = r.nz ? hz : lz, bz = r.nz ? lz : hz;
+    const float tix = (ax - r.o.x) * r.rcp.x, tiy = (ay - r.o.y) * r.rcp.y, tiz = (az - r.o.z) * r.rcp.z;
+    const float tox = (bx - r.o.x) * r.rcp.x, toy = (by - r.o.y) * r.rcp.y, toz = (bz - r.o.z) * r.rcp.z;
+    const float tin = smax(tix, smax(tiy, tiz));
+    const float tout = smin(tox, smin(toy, toz));
+    return (tout >= 0.0f) && (tin <= tout);
+}
+
+// Whitted::RayTriangleIntersection, MC/TriangleMesh.h:19-45 (float cross/dot, double reciprocal
+// and barycentrics, strict inequalities).  A float sign pre-test rejects exactly the cases whose
+// double products cannot all be positive; a conservative |b2+b3| > |den| screen rejects cases the
+// double test would reject too; survivors run the reference's double arithmetic unchanged.
+__device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
+{
+    const V3 S = sub(r.o, a);
+    const V3 S1 = cross(r.d, e2), S2 = cross(S, e1);
+    const float den = dot(S1, e1);
+    const float tn = dot(S2, e2), b2n = dot(S1, S), b3n = dot(S2, r.d);
+    const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
+    const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
+    if (!(pos || ngt)) return false;
+    if ((__builtin_fabsf(b2n) + __builtin_fabsf(b3n)) > __builtin_fabsf(den) * 1.00001f) return false;
+    const double inv = 1.0 / (double)den;
+    const double t = (double)tn * inv;
+    const double b2 = (double)b2n * inv;
+    const double b3 = (double)b3n * inv;
+    t_out = t;
+    return (t > 0.0) && (b2 > 0.0) && (b3 > 0.0) && (((1.0 - b2) - b3) > 0.0);
+}
+
+// cos/sin of the hemisphere angle: double evaluation, one rounding (see header)
+__device__ __forceinline__ float cos_f(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float sin_f(float x) { return (float)sin((double)x); }
+
+// glm mat4 * vec4, GLM/detail/type_mat4x4.inl:561-572: (m0*v0 + m1*v1) + (m2*v2 + m3*v3); m column-major
+__device__ __forceinline__ void mat4_mul(const float* m, float v0, float v1, float v2, float v3, float out[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float mul0 = m[0 + i] * v0, mul1 = m[4 + i] * v1, mul2 = m[8 + i] * v2, mul3 = m[12 + i] * v3;
+        const float add0 = mul0 + mul1, add1 = mul2 + mul3;
+        out[i] = add0 + add1;
+    }
+}
+
+}  // namespace rtd
+#endif

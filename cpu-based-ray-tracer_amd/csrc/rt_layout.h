@@ -1,0 +1,41 @@
+// rt_layout.h -- device-side scene layout shared by the host builder (rt_scene.cpp) and the
+// HIP kernels (rt_kernels.hip).  Plain C structs, no HIP types.
+//
+// HBM layout (all arrays 16-byte aligned, float4-granular):
+//
+//  nodes   : 2 x float4 per BVH node, flattened two-level BVH in DFS pre-order
+//            (top-level BVH over meshes, each top-level leaf replaced by the mesh's own BVH root;
+//            exact because a mesh's top-level box equals its mesh-root box,
+//            MC/TriangleMesh.h:173-178 vs MC/BVH.h:155,208).
+//              q0 = (lo.x, lo.y, lo.z, hi.x)
+//              q1 = (hi.y, hi.z, bits(skip), bits(tri))
+//            skip = index of the next node in DFS pre-order after this node's subtree (== count at
+//            the end); tri = triangle slot for leaves, -1 for internal nodes.  An internal node's
+//            left child is the next node (i+1).  A miss or a finished leaf continues at `skip`,
+//            so a stackless walk visits exactly the nodes the reference's recursion visits
+//            (BVH::traverse_BVH_from_node, MC/BVH.h:82-101).
+//  tris    : 4 x float4 per triangle, in DFS leaf order (slot == flattened leaf index)
+//              q0 = (a.xyz, bits(material)), q1 = (e1 = b-a, 0), q2 = (e2 = c-a, 0), q3 = (n.xyz, 0)
+//            (Moller-Trumbore reads q0..q2 = 48 B; shading reads q3)
+//  mats    : 2 x float4 per material: (brdf = albedo/PI, emitting), (emission, 0)
+//  lnodes  : light-mesh BVH for area sampling (BVH::Sampling_from_node, MC/BVH.h:114-129):
+//            1 x float4 per node (area, bits(left), bits(right), bits(light_tri)), root = 0
+//  ltris   : 4 x float4 per light triangle: (a, 0), (b, 0), (c, 0), (n, area)
+#ifndef RT_LAYOUT_H
+#define RT_LAYOUT_H
+#include <stdint.h>
+
+#define RT_NODE_QUADS 2
+#define RT_TRI_QUADS 4
+#define RT_MAT_QUADS 2
+#define RT_LTRI_QUADS 4
+
+typedef struct {
+    uint32_t n_nodes, n_tris, n_mats, n_lnodes, n_ltris;
+    int32_t light_mesh;        // first emissive mesh in insertion order (MC/Renderer.h:169-179), -1 if none
+    float light_area;          // light mesh BVH root mesh_area (pdf = 1/area, MC/BVH.h:106)
+    float light_emission[3];   // emission of the light mesh material (MC/TriangleMesh.h:195)
+    uint32_t max_depth;        // deepest node level (for diagnostics)
+} rt_scene_header;
+
+#endif

@@ -1,0 +1,234 @@
+// rt_renderer.cpp -- the C++20 drop-in classes (include/rt/Renderer.h, include/rt/Camera.h) on top of
+// the C-ABI.  Reference: MC/Renderer.{h,cpp}, MC/Camera.{h,cpp}.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "rt/Renderer.h"
+#include "rt_camera.h"
+#include "rt_scene.h"
+
+// ============================================================================ Camera
+Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance)
+    : vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance}, far_clip_plane_distance{FarClipPlaneDistance}
+{
+}
+
+void Camera::RecomputeProjectionMatrix()
+{   // MC/Camera.cpp:101-105
+    const float p[3] = {position.x, position.y, position.z}, f[3] = {forward_direction.x, forward_direction.y, forward_direction.z};
+    rt::camera_matrices(viewport_width, viewport_height, p, f, vertical_FOV, near_clip_plane_distance, far_clip_plane_distance,
+                        projection_matrix.m.data(), inverse_projection_matrix.m.data(), nullptr, nullptr);
+}
+
+void Camera::RecomputeViewMatrix()
+{   // MC/Camera.cpp:107-112
+    const float p[3] = {position.x, position.y, position.z}, f[3] = {forward_direction.x, forward_direction.y, forward_direction.z};
+    rt::camera_matrices(viewport_width ? viewport_width : 1, viewport_height ? viewport_height : 1, p, f, vertical_FOV,
+                        near_clip_plane_distance, far_clip_plane_distance, nullptr, nullptr, view_matrix.m.data(), inverse_view_matrix.m.data());
+    ray_directions.clear();
+}
+
+void Camera::ResizeViewport(uint32_t new_width, uint32_t new_height)
+{   // MC/Camera.cpp:87-99
+    if (viewport_width == new_width && viewport_height == new_height) return;
+    viewport_width = new_width;
+    viewport_height = new_height;
+    RecomputeProjectionMatrix();
+    RecomputeViewMatrix();
+}
+
+bool Camera::UpdateCamera(float dt)
+{
+    rt::CameraInput none;
+    return UpdateCamera(dt, none);
+}
+
+bool Camera::UpdateCamera(float dt, const rt::CameraInput& in)
+{   // MC/Camera.cpp:24-85 (input from the caller instead of Walnut::Input)
+    RecomputeViewMatrix();
+    if (!in.rotating) return false;
+    bool moved = false;
+    const float speed = 5.0f;
+    auto cross = [](rt::vec3 a, rt::vec3 b) { return rt::vec3{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; };
+    const rt::vec3 right = cross(forward_direction, up_direction);
+    auto step = [&](rt::vec3 d, float s) { position.x += s * d.x; position.y += s * d.y; position.z += s * d.z; moved = true; };
+    if (in.forward) step(forward_direction, speed * dt);
+    if (in.back) step(forward_direction, -speed * dt);
+    if (in.right) step(right, speed * dt);
+    if (in.left) step(right, -speed * dt);
+    if (in.up) step(up_direction, speed * dt);
+    if (in.down) step(up_direction, -speed * dt);
+    if (in.mouse_dx != 0.0f || in.mouse_dy != 0.0f) {
+        // q = normalize(angleAxis(-pitch, right) x angleAxis(-yaw, up)); forward = rotate(q, forward)
+        const float pitch = in.mouse_dy * Sensitivity(), yaw = in.mouse_dx * Sensitivity();
+        const float ha = -pitch * 0.5f, hb = -yaw * 0.5f;
+        const float aw = std::cos(ha), as = std::sin(ha), bw = std::cos(hb), bs = std::sin(hb);
+        const float ax = right.x * as, ay = right.y * as, az = right.z * as;
+        const float bx = up_direction.x * bs, by = up_direction.y * bs, bz = up_direction.z * bs;
+        float qw = aw * bw - (ax * bx + ay * by + az * bz);
+        float qx = aw * bx + bw * ax + (ay * bz - az * by);
+        float qy = aw * by + bw * ay + (az * bx - ax * bz);
+        float qz = aw * bz + bw * az + (ax * by - ay * bx);
+        const float n = std::sqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+        qw /= n; qx /= n; qy /= n; qz /= n;
+        const rt::vec3 v = forward_direction;
+        const rt::vec3 qv{qx, qy, qz};
+        const rt::vec3 uv = cross(qv, v), uuv = cross(qv, uv);
+        forward_direction = rt::vec3{v.x + 2.0f * (uv.x * qw + uuv.x), v.y + 2.0f * (uv.y * qw + uuv.y), v.z + 2.0f * (uv.z * qw + uuv.z)};
+        moved = true;
+    }
+    if (moved) RecomputeViewMatrix();
+    return moved;
+}
+
+rt_camera Camera::Native() const
+{
+    rt_camera c;
+    c.position[0] = position.x; c.position[1] = position.y; c.position[2] = position.z;
+    std::memcpy(c.inv_projection, inverse_projection_matrix.m.data(), 64);
+    std::memcpy(c.inv_view, inverse_view_matrix.m.data(), 64);
+    return c;
+}
+
+namespace {
+// host copy of the frozen RNG stream (the kernel's rtd::Rng): Philox4x32-10
+uint32_t rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim)
+{
+    uint32_t c0 = pixel, c1 = frame, c2 = dim >> 2, c3 = 0, k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    const uint32_t o[4] = {c0, c1, c2, c3};
+    return o[dim & 3u];
+}
+}  // namespace
+
+const std::vector<rt::vec3>& Camera::RayDirections(uint32_t frame, uint64_t seed) const
+{   // RecomputeRayDirections, MC/Camera.cpp:114-132, for one frame of the kernel's RNG stream
+    const uint32_t W = viewport_width, H = viewport_height;
+    ray_directions.resize((size_t)W * H);
+    const float* ip = inverse_projection_matrix.m.data();
+    const float* iv = inverse_view_matrix.m.data();
+    auto mul = [](const float* m, float v0, float v1, float v2, float v3, float* o) {
+        for (int i = 0; i < 4; ++i) { const float a = m[i] * v0, b = m[4 + i] * v1, c = m[8 + i] * v2, d = m[12 + i] * v3; o[i] = (a + b) + (c + d); }
+    };
+    for (uint32_t y = 0; y < H; ++y)
+        for (uint32_t x = 0; x < W; ++x) {
+            const uint32_t px = y * W + x;
+            const float ux = (float)rng_u32(seed, px, frame, 0) / 4294967296.0f, uy = (float)rng_u32(seed, px, frame, 1) / 4294967296.0f;
+            float cx = ((float)x + ux) / (float)W, cy = ((float)y + uy) / (float)H;
+            cx = cx * 2.0f - 1.0f; cy = cy * 2.0f - 1.0f;
+            float t[4], w[4];
+            mul(ip, cx, cy, 1.0f, 1.0f, t);
+            float d[3] = {t[0] / t[3], t[1] / t[3], t[2] / t[3]};
+            const float dd = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+            const float s = 1.0f / std::sqrt(dd);
+            mul(iv, d[0] * s, d[1] * s, d[2] * s, 0.0f, w);
+            ray_directions[px] = rt::vec3{w[0], w[1], w[2]};
+        }
+    return ray_directions;
+}
+
+// ============================================================================ entities
+rt::TriangleMesh::TriangleMesh(const std::string& file_path, const Material& m) : material_(m)
+{
+    std::string err;
+    if (!rt::SceneBuilder::load_obj_positions(file_path, raw_, err)) throw rt::Error("TriangleMesh: " + err);
+}
+
+rt::TriangleMesh::TriangleMesh(std::vector<float> raw_positions, const Material& m) : raw_(std::move(raw_positions)), material_(m) {}
+
+// ============================================================================ Renderer
+void Renderer::check(rt_status s, const char* what) const
+{
+    if (s != RT_OK) throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
+}
+
+Renderer::Renderer() : Renderer(Settings{}, true) {}
+
+Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
+{
+    rt_device_cfg cfg{settings.device, nullptr, 0};
+    check(rt_create(&ctx, &cfg), "rt_create");
+    if (cornell_box) {
+        // Renderer::Renderer(): materials + six meshes + GenerateBVH (MC/Renderer.cpp:26-57)
+        for (auto& m : rt::SceneBuilder::cornell_box_meshes()) {
+            rt::Material mat;
+            mat.diffuse_coefficient = rt::vec3{m.material.albedo.x, m.material.albedo.y, m.material.albedo.z};
+            mat.emission = rt::vec3{m.material.emission.x, m.material.emission.y, m.material.emission.z};
+            owned.push_back(std::make_unique<rt::TriangleMesh>(std::move(m.raw), mat));
+            Add(owned.back().get());
+        }
+        GenerateBVH();
+    }
+}
+
+Renderer::~Renderer() { rt_destroy(ctx); }
+
+void Renderer::GenerateBVH()
+{
+    rt_scene* sc = nullptr;
+    check(rt_scene_create(&sc), "rt_scene_create");
+    for (rt::Entity* e : entities) {
+        const auto& raw = e->RawPositions();
+        const rt::Material& m = e->GetMaterial();
+        const float alb[3] = {m.diffuse_coefficient.x, m.diffuse_coefficient.y, m.diffuse_coefficient.z};
+        const float em[3] = {m.emission.x, m.emission.y, m.emission.z};
+        rt_status st = rt_scene_add_mesh(sc, raw.data(), raw.size() / 9, alb, em, nullptr);
+        if (st != RT_OK) { rt_scene_destroy(sc); check(st, "rt_scene_add_mesh"); }
+    }
+    rt_status st = rt_scene_build(sc);
+    if (st == RT_OK) st = rt_upload_scene(ctx, sc);
+    rt_scene_destroy(sc);
+    check(st, "GenerateBVH");
+    bvh_dirty = false;
+}
+
+void Renderer::ResizeViewport(uint32_t width, uint32_t height)
+{   // MC/Renderer.cpp:59-89
+    if (frame_image_final) {
+        if (frame_image_final->GetWidth() == width && frame_image_final->GetHeight() == height) return;
+        frame_image_final->Resize(width, height);
+    } else {
+        frame_image_final = std::make_shared<rt::Image>(width, height);
+    }
+    check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
+    frame_accumulating = 1;
+}
+
+void Renderer::Render(const Camera& camera) { RenderFrames(camera, 1); }
+
+void Renderer::RenderFrames(const Camera& camera, uint32_t n)
+{   // MC/Renderer.cpp:91-122, n frames per launch
+    if (!frame_image_final) throw rt::Error("Render before ResizeViewport");
+    if (bvh_dirty) GenerateBVH();
+    const rt_camera cam = camera.Native();
+    rt_render_params p{frame_accumulating, n, settings.seed + epoch, RR_survival_probability, settings.exact ? RT_RENDER_EXACT : 0u};
+    check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
+    if (settings.accumulating) frame_accumulating += n;
+    else frame_accumulating = 1;
+}
+
+const std::vector<float>& Renderer::GetAccumulation()
+{
+    void* d_acc = nullptr;
+    check(rt_device_buffers(ctx, &d_acc, nullptr), "rt_device_buffers");
+    const size_t n = frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0;
+    accum_host.resize(n);
+    // a render with a host pointer synchronises; this re-reads the device buffer
+    rt_render_params p{frame_accumulating, 0, settings.seed + epoch, RR_survival_probability, 0};
+    const rt_camera cam{};
+    check(rt_render(ctx, &cam, &p, nullptr, accum_host.data()), "read accumulation");
+    return accum_host;
+}
+
+float Renderer::LastKernelMilliseconds() const
+{
+    rt_stats st{};
+    if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
+    return st.last_kernel_ms;
+}

@@ -1,0 +1,405 @@
+// rt_scene.cpp -- host scene path (see rt_scene.h).
+//
+// Reference anchors (MC/ = "Monte Carlo Path Tracer/8599RayTracerGUI/src/"):
+//   OBJ records          objl::Loader::LoadFile / GenVerticesFromRawOBJ, MC/OBJ_Loader.h:434-842
+//   mesh construction    Whitted::TriangleMesh::TriangleMesh, MC/TriangleMesh.h:148-186 (x0.01 scale)
+//   triangle             Whitted::TrianglePrimitive ctor / Get3DAABB, MC/TriangleMesh.h:54-60,96-99
+//   BVH build            AccelerationStructure::BVH::build_BVH, MC/BVH.h:131-214 (median split,
+//                        std::sort on the centroid along the longest centroid axis)
+//   boxes                AABB_3D, MC/BoundingVolume.h:32-45,116-171
+// Every float expression keeps the reference's (glm 0.9.9.9's) operation order; the tree and the
+// numbers are checked bit-exactly against tests/golden/cornell_scene.npz.
+#include "rt_scene.h"
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <cmath>
+#include <fstream>
+#include <limits>
+#include <sstream>
+
+namespace rt {
+namespace {
+
+inline F3 sub(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline F3 cross(F3 x, F3 y) { return F3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+inline float dot(F3 a, F3 b) { float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return tx + ty + tz; }
+inline float gmin(float x, float y) { return (y < x) ? y : x; }   // glm::min / std::min
+inline float gmax(float x, float y) { return (x < y) ? y : x; }   // glm::max / std::max
+inline float bits_as_float(int32_t i) { float f; std::memcpy(&f, &i, 4); return f; }
+
+struct Box { F3 lo, hi; };
+inline Box box_union(const Box& a, const Box& b)
+{
+    return Box{F3{gmin(a.lo.x, b.lo.x), gmin(a.lo.y, b.lo.y), gmin(a.lo.z, b.lo.z)},
+               F3{gmax(a.hi.x, b.hi.x), gmax(a.hi.y, b.hi.y), gmax(a.hi.z, b.hi.z)}};
+}
+inline F3 centre(const Box& b)
+{   // center_vector: 0.5f * (max + min)
+    return F3{0.5f * (b.hi.x + b.lo.x), 0.5f * (b.hi.y + b.lo.y), 0.5f * (b.hi.z + b.lo.z)};
+}
+
+struct Tri {
+    F3 a, b, c, n;
+    float area;
+    Box box;
+    int mesh;
+};
+
+// A built (unflattened) binary tree; leaves reference an item id.
+struct BNode { Box box; float area; int left = -1, right = -1, item = -1; };
+
+struct Item { Box box; float area; F3 c; int id; };
+
+int build_bvh(std::vector<BNode>& nodes, std::vector<Item>& items, size_t lo, size_t hi)
+{
+    const size_t n = hi - lo;
+    const int me = (int)nodes.size();
+    nodes.emplace_back();
+    if (n == 1) {
+        nodes[me].box = items[lo].box; nodes[me].area = items[lo].area; nodes[me].item = items[lo].id;
+        return me;
+    }
+    size_t mid;
+    if (n == 2) {
+        mid = lo + 1;   // two entities: no sort (MC/BVH.h:150-158)
+    } else {
+        // centroid bounds start from the empty box (double max -> +inf as float, MC/BoundingVolume.h:32-39)
+        const float inf = (float)std::numeric_limits<double>::max();
+        Box cb{F3{inf, inf, inf}, F3{-inf, -inf, -inf}};
+        for (size_t i = lo; i < hi; ++i) {
+            const F3 p = items[i].c;
+            cb = Box{F3{gmin(cb.lo.x, p.x), gmin(cb.lo.y, p.y), gmin(cb.lo.z, p.z)}, F3{gmax(cb.hi.x, p.x), gmax(cb.hi.y, p.y), gmax(cb.hi.z, p.z)}};
+        }
+        const F3 d = sub(cb.hi, cb.lo);
+        int axis = ((d.x > d.y) && (d.x > d.z)) ? 0 : (d.y > d.z ? 1 : 2);   // longest_axis
+        auto first = items.begin() + (std::ptrdiff_t)lo, last = items.begin() + (std::ptrdiff_t)hi;
+        // std::sort (introsort) with the reference's strict comparator; sorting the sub-range in place
+        // performs the same comparisons as the reference's sort of its copied half.
+        if (axis == 0) std::sort(first, last, [](const Item& a, const Item& b) { return a.c.x < b.c.x; });
+        else if (axis == 1) std::sort(first, last, [](const Item& a, const Item& b) { return a.c.y < b.c.y; });
+        else std::sort(first, last, [](const Item& a, const Item& b) { return a.c.z < b.c.z; });
+        mid = lo + n / 2;
+    }
+    const int l = build_bvh(nodes, items, lo, mid);
+    const int r = build_bvh(nodes, items, mid, hi);
+    nodes[me].left = l; nodes[me].right = r;
+    nodes[me].box = box_union(nodes[l].box, nodes[r].box);
+    nodes[me].area = nodes[l].area + nodes[r].area;
+    return me;
+}
+
+// objl helpers (MC/OBJ_Loader.h:324-398)
+std::string first_token(const std::string& in)
+{
+    if (in.empty()) return "";
+    size_t a = in.find_first_not_of(" \t");
+    if (a == std::string::npos) return "";
+    size_t b = in.find_first_of(" \t", a);
+    return b == std::string::npos ? in.substr(a) : in.substr(a, b - a);
+}
+std::string tail(const std::string& in)
+{
+    size_t ts = in.find_first_not_of(" \t");
+    size_t ss = in.find_first_of(" \t", ts);
+    size_t ta = in.find_first_not_of(" \t", ss);
+    size_t te = in.find_last_not_of(" \t");
+    if (ta != std::string::npos && te != std::string::npos) return in.substr(ta, te - ta + 1);
+    if (ta != std::string::npos) return in.substr(ta);
+    return "";
+}
+std::vector<std::string> split_on(const std::string& in, char tok)
+{   // objl::algorithm::split with a one-character token: empty fields are kept, trailing token dropped
+    std::vector<std::string> out;
+    std::string cur;
+    for (size_t i = 0; i < in.size(); ++i) {
+        if (in[i] == tok) {
+            out.push_back(cur);
+            cur.clear();
+        } else {
+            cur += in[i];
+            if (i + 1 == in.size()) out.push_back(cur);
+        }
+    }
+    return out;
+}
+
+}  // namespace
+
+bool SceneBuilder::load_obj_positions(const std::string& path, std::vector<float>& raw, std::string& err)
+{
+    raw.clear();
+    if (path.size() < 4 || path.substr(path.size() - 4) != ".obj") { err = "not an .obj file: " + path; return false; }
+    std::ifstream f(path);
+    if (!f.is_open()) { err = "cannot open " + path; return false; }
+    std::vector<F3> pos;
+    std::string line;
+    int groups = 0;
+    while (std::getline(f, line)) {
+        const std::string ft = first_token(line);
+        if (ft == "v") {
+            auto sp = split_on(tail(line), ' ');
+            if (sp.size() < 3) { err = "bad v record"; return false; }
+            pos.push_back(F3{std::stof(sp[0]), std::stof(sp[1]), std::stof(sp[2])});
+        } else if (ft == "f") {
+            for (const auto& s : split_on(tail(line), ' ')) {
+                auto sv = split_on(s, '/');
+                if (sv.empty() || sv.size() > 3 || sv[0].empty()) continue;
+                int idx = std::stoi(sv[0]);
+                idx = idx < 0 ? (int)pos.size() + idx : idx - 1;   // objl::algorithm::getElement
+                if (idx < 0 || idx >= (int)pos.size()) { err = "face index out of range"; return false; }
+                raw.push_back(pos[idx].x); raw.push_back(pos[idx].y); raw.push_back(pos[idx].z);
+            }
+        } else if (ft == "o" || ft == "g") {
+            // a second object would start objl's second mesh; TriangleMesh asserts a single mesh
+            // (MC/TriangleMesh.h:158)
+            if (!raw.empty() && ++groups > 0) { err = "multi-mesh OBJ files are not supported (TriangleMesh asserts one mesh)"; return false; }
+        }
+    }
+    // TriangleMesh consumes Vertices three at a time (MC/TriangleMesh.h:165); a ragged tail is ignored
+    raw.resize(raw.size() - raw.size() % 9);
+    return true;
+}
+
+void SceneBuilder::add_cornell_box()
+{
+    for (auto& m : cornell_box_meshes()) add_mesh(std::move(m));
+}
+
+std::vector<MeshDesc> SceneBuilder::cornell_box_meshes()
+{
+    std::vector<MeshDesc> out;
+    // Cornell box measurement data (http://www.graphics.cornell.edu/online/box/data.html), laid out
+    // as the reference's cornellbox/*.obj: vertex lists + 1-based faces, millimetres.
+    struct Raw { const char* name; std::vector<F3> v; std::vector<int> f; MaterialDesc m; };
+    const MaterialDesc red{{0.63f, 0.065f, 0.05f}, {0, 0, 0}}, green{{0.1f, 0.5f, 0.1f}, {0, 0, 0}},
+        white{{0.7f, 0.7f, 0.7f}, {0, 0, 0}}, light{{0.7f, 0.7f, 0.7f}, {47.8f, 38.6f, 31.1f}};   // MC/Renderer.cpp:28-35
+    const std::vector<int> quad{1, 2, 3, 1, 3, 4};
+    std::vector<int> box_faces;
+    for (int k = 0; k < 5; ++k) for (int j : quad) box_faces.push_back(4 * k + j);
+    const Raw meshes[6] = {
+        {"floor", {{552.8f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 559.2f}, {549.6f, 0.0f, 559.2f},
+                   {556.0f, 548.8f, 0.0f}, {556.0f, 548.8f, 559.2f}, {0.0f, 548.8f, 559.2f}, {0.0f, 548.8f, 0.0f},
+                   {549.6f, 0.0f, 559.2f}, {0.0f, 0.0f, 559.2f}, {0.0f, 548.8f, 559.2f}, {556.0f, 548.8f, 559.2f}},
+         {1, 2, 3, 3, 4, 1, 5, 6, 7, 7, 8, 5, 9, 10, 11, 11, 12, 9}, white},
+        {"shortbox", {{130.0f, 165.0f, 65.0f}, {82.0f, 165.0f, 225.0f}, {240.0f, 165.0f, 272.0f}, {290.0f, 165.0f, 114.0f},
+                      {290.0f, 0.0f, 114.0f}, {290.0f, 165.0f, 114.0f}, {240.0f, 165.0f, 272.0f}, {240.0f, 0.0f, 272.0f},
+                      {130.0f, 0.0f, 65.0f}, {130.0f, 165.0f, 65.0f}, {290.0f, 165.0f, 114.0f}, {290.0f, 0.0f, 114.0f},
+                      {82.0f, 0.0f, 225.0f}, {82.0f, 165.0f, 225.0f}, {130.0f, 165.0f, 65.0f}, {130.0f, 0.0f, 65.0f},
+                      {240.0f, 0.0f, 272.0f}, {240.0f, 165.0f, 272.0f}, {82.0f, 165.0f, 225.0f}, {82.0f, 0.0f, 225.0f}},
+         box_faces, white},
+        {"tallbox", {{423.0f, 330.0f, 247.0f}, {265.0f, 330.0f, 296.0f}, {314.0f, 330.0f, 456.0f}, {472.0f, 330.0f, 406.0f},
+                     {423.0f, 0.0f, 247.0f}, {423.0f, 330.0f, 247.0f}, {472.0f, 330.0f, 406.0f}, {472.0f, 0.0f, 406.0f},
+                     {472.0f, 0.0f, 406.0f}, {472.0f, 330.0f, 406.0f}, {314.0f, 330.0f, 456.0f}, {314.0f, 0.0f, 456.0f},
+                     {314.0f, 0.0f, 456.0f}, {314.0f, 330.0f, 456.0f}, {265.0f, 330.0f, 296.0f}, {265.0f, 0.0f, 296.0f},
+                     {265.0f, 0.0f, 296.0f}, {265.0f, 330.0f, 296.0f}, {423.0f, 330.0f, 247.0f}, {423.0f, 0.0f, 247.0f}},
+         box_faces, white},
+        {"left", {{552.8f, 0.0f, 0.0f}, {549.6f, 0.0f, 559.2f}, {556.0f, 548.8f, 559.2f}, {556.0f, 548.8f, 0.0f}}, quad, red},
+        {"right", {{0.0f, 0.0f, 559.2f}, {0.0f, 0.0f, 0.0f}, {0.0f, 548.8f, 0.0f}, {0.0f, 548.8f, 559.2f}}, quad, green},
+        {"light", {{343.0f, 548.7f, 227.0f}, {343.0f, 548.7f, 332.0f}, {213.0f, 548.7f, 332.0f}, {213.0f, 548.7f, 227.0f}}, quad, light},
+    };
+    for (const auto& m : meshes) {
+        MeshDesc d;
+        d.name = m.name;
+        d.material = m.m;
+        for (int idx : m.f) { const F3& p = m.v[idx - 1]; d.raw.push_back(p.x); d.raw.push_back(p.y); d.raw.push_back(p.z); }
+        out.push_back(std::move(d));
+    }
+    return out;
+}
+
+int SceneBuilder::add_mesh(MeshDesc m)
+{
+    meshes_.push_back(std::move(m));
+    return (int)meshes_.size() - 1;
+}
+
+bool SceneBuilder::build(FlatScene& out, std::string& err) const
+{
+    out = FlatScene{};
+    const size_t nm = meshes_.size();
+    if (nm == 0) { err = "empty scene"; return false; }
+    // ---- per mesh: triangles, mesh box, total area, mesh BVH (TriangleMesh ctor)
+    std::vector<std::vector<Tri>> tris(nm);
+    std::vector<std::vector<BNode>> mesh_nodes(nm);
+    std::vector<int> mesh_root(nm, -1);
+    std::vector<Box> mesh_box(nm);
+    std::vector<float> mesh_area(nm, 0.0f);
+    for (size_t mi = 0; mi < nm; ++mi) {
+        const auto& raw = meshes_[mi].raw;
+        const size_t nt = raw.size() / 9;
+        if (nt == 0) { err = "mesh without triangles: " + meshes_[mi].name; return false; }
+        const float inf = std::numeric_limits<float>::infinity();
+        F3 rmin{inf, inf, inf}, rmax{-inf, -inf, -inf};
+        for (size_t t = 0; t < nt; ++t) {
+            F3 v[3];
+            for (int j = 0; j < 3; ++j) {
+                const float* q = &raw[9 * t + 3 * j];
+                v[j] = F3{0.01f * q[0], 0.01f * q[1], 0.01f * q[2]};   // mesh_scale * vec3
+                rmin = F3{std::min(rmin.x, v[j].x), std::min(rmin.y, v[j].y), std::min(rmin.z, v[j].z)};
+                rmax = F3{std::max(rmax.x, v[j].x), std::max(rmax.y, v[j].y), std::max(rmax.z, v[j].z)};
+            }
+            Tri tr;
+            tr.a = v[0]; tr.b = v[1]; tr.c = v[2]; tr.mesh = (int)mi;
+            const F3 cp = cross(sub(tr.b, tr.a), sub(tr.c, tr.a));
+            tr.area = 0.5f * std::sqrt(dot(cp, cp));
+            const float l2 = cp.x * cp.x + cp.y * cp.y + cp.z * cp.z;   // Whitted::normalize (zero-safe)
+            if (l2 > 0) { const float inv = 1 / std::sqrt(l2); tr.n = F3{cp.x * inv, cp.y * inv, cp.z * inv}; }
+            else tr.n = cp;
+            const Box ab{F3{std::fmin(tr.a.x, tr.b.x), std::fmin(tr.a.y, tr.b.y), std::fmin(tr.a.z, tr.b.z)},
+                         F3{std::fmax(tr.a.x, tr.b.x), std::fmax(tr.a.y, tr.b.y), std::fmax(tr.a.z, tr.b.z)}};
+            tr.box = Box{F3{gmin(ab.lo.x, tr.c.x), gmin(ab.lo.y, tr.c.y), gmin(ab.lo.z, tr.c.z)},
+                         F3{gmax(ab.hi.x, tr.c.x), gmax(ab.hi.y, tr.c.y), gmax(ab.hi.z, tr.c.z)}};
+            tris[mi].push_back(tr);
+        }
+        mesh_box[mi] = Box{F3{std::fmin(rmin.x, rmax.x), std::fmin(rmin.y, rmax.y), std::fmin(rmin.z, rmax.z)},
+                           F3{std::fmax(rmin.x, rmax.x), std::fmax(rmin.y, rmax.y), std::fmax(rmin.z, rmax.z)}};
+        std::vector<Item> items;
+        for (size_t t = 0; t < nt; ++t) {
+            mesh_area[mi] += tris[mi][t].area;
+            items.push_back(Item{tris[mi][t].box, tris[mi][t].area, centre(tris[mi][t].box), (int)t});
+        }
+        mesh_root[mi] = build_bvh(mesh_nodes[mi], items, 0, items.size());
+    }
+    // ---- top level: BVH over meshes (entity box = mesh box, area = total_area)
+    std::vector<BNode> top;
+    std::vector<Item> titems;
+    for (size_t mi = 0; mi < nm; ++mi) titems.push_back(Item{mesh_box[mi], mesh_area[mi], centre(mesh_box[mi]), (int)mi});
+    const int top_root = build_bvh(top, titems, 0, titems.size());
+
+    // ---- flatten: DFS pre-order, top leaves replaced by mesh roots
+    struct FN { Box box; float area; int tri; int mesh; int top; int skip; int left, right; };
+    std::vector<FN> fn;
+    std::vector<const Tri*> slot_tri;
+    std::vector<std::pair<int, int>> slot_src;   // (mesh, local tri)
+    std::function<int(int, int)> walk_mesh = [&](int mi, int ni) -> int {
+        const BNode& b = mesh_nodes[mi][ni];
+        const int me = (int)fn.size();
+        fn.push_back(FN{b.box, b.area, -1, mi, 0, -1, -1, -1});
+        if (b.left < 0) {
+            fn[me].tri = (int)slot_tri.size();
+            slot_tri.push_back(&tris[mi][b.item]);
+            slot_src.emplace_back(mi, b.item);
+        } else {
+            const int l = walk_mesh(mi, b.left);
+            const int r = walk_mesh(mi, b.right);
+            fn[me].left = l; fn[me].right = r;
+        }
+        fn[me].skip = (int)fn.size();
+        return me;
+    };
+    std::function<int(int)> walk_top = [&](int ni) -> int {
+        const BNode& b = top[ni];
+        if (b.left < 0) {
+            const int mi = b.item;
+            // a top-level leaf box is the mesh box; it must equal the mesh-root box for the flattening
+            const Box& mb = mesh_nodes[mi][mesh_root[mi]].box;
+            if (std::memcmp(&mb, &b.box, sizeof(Box)) != 0) { err = "mesh box != mesh root box"; return -1; }
+            return walk_mesh(mi, mesh_root[mi]);
+        }
+        const int me = (int)fn.size();
+        fn.push_back(FN{b.box, b.area, -1, -1, 1, -1, -1, -1});
+        const int l = walk_top(b.left);
+        const int r = walk_top(b.right);
+        if (l < 0 || r < 0) return -1;
+        fn[me].left = l; fn[me].right = r;
+        fn[me].skip = (int)fn.size();
+        return me;
+    };
+    if (walk_top(top_root) < 0) return false;
+
+    const uint32_t NN = (uint32_t)fn.size(), NT = (uint32_t)slot_tri.size();
+    out.nodes.resize((size_t)NN * 8);
+    out.dbg_node_f.resize((size_t)NN * 7);
+    out.dbg_node_i.resize((size_t)NN * 5);
+    for (uint32_t i = 0; i < NN; ++i) {
+        const FN& n = fn[i];
+        float* q = &out.nodes[8 * (size_t)i];
+        q[0] = n.box.lo.x; q[1] = n.box.lo.y; q[2] = n.box.lo.z; q[3] = n.box.hi.x;
+        q[4] = n.box.hi.y; q[5] = n.box.hi.z; q[6] = bits_as_float(n.skip); q[7] = bits_as_float(n.tri);
+        float* d = &out.dbg_node_f[7 * (size_t)i];
+        d[0] = n.box.lo.x; d[1] = n.box.lo.y; d[2] = n.box.lo.z; d[3] = n.box.hi.x; d[4] = n.box.hi.y; d[5] = n.box.hi.z; d[6] = n.area;
+        int32_t* e = &out.dbg_node_i[5 * (size_t)i];
+        e[0] = n.left; e[1] = n.right; e[2] = n.tri; e[3] = n.mesh; e[4] = n.top;
+    }
+    out.tris.resize((size_t)NT * 16);
+    out.dbg_tri_f.resize((size_t)NT * 13);
+    out.dbg_tri_i.resize((size_t)NT * 2);
+    for (uint32_t s = 0; s < NT; ++s) {
+        const Tri& t = *slot_tri[s];
+        const F3 e1 = sub(t.b, t.a), e2 = sub(t.c, t.a);
+        float* q = &out.tris[16 * (size_t)s];
+        q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = bits_as_float(t.mesh);   // material id == mesh id
+        q[4] = e1.x; q[5] = e1.y; q[6] = e1.z; q[7] = 0.0f;
+        q[8] = e2.x; q[9] = e2.y; q[10] = e2.z; q[11] = 0.0f;
+        q[12] = t.n.x; q[13] = t.n.y; q[14] = t.n.z; q[15] = 0.0f;
+        float* d = &out.dbg_tri_f[13 * (size_t)s];
+        const F3 vv[4] = {t.a, t.b, t.c, t.n};
+        for (int k = 0; k < 4; ++k) { d[3 * k] = vv[k].x; d[3 * k + 1] = vv[k].y; d[3 * k + 2] = vv[k].z; }
+        d[12] = t.area;
+        out.dbg_tri_i[2 * s] = t.mesh; out.dbg_tri_i[2 * s + 1] = t.mesh;
+    }
+    // ---- materials (one per mesh): brdf = diffuse_coefficient / PI, emitting = length(emission) > 1e-5
+    const float PI = 3.141592653589793f;   // MC/WhittedUtilities.h:20
+    out.mats.resize(nm * 8);
+    int light = -1;
+    for (size_t mi = 0; mi < nm; ++mi) {
+        const MaterialDesc& m = meshes_[mi].material;
+        const bool emitting = std::sqrt(dot(m.emission, m.emission)) > 0.00001f;   // MC/WhittedMaterial.h:34
+        if (emitting && light < 0) light = (int)mi;
+        float* q = &out.mats[8 * mi];
+        q[0] = m.albedo.x / PI; q[1] = m.albedo.y / PI; q[2] = m.albedo.z / PI; q[3] = emitting ? 1.0f : 0.0f;
+        q[4] = m.emission.x; q[5] = m.emission.y; q[6] = m.emission.z; q[7] = 0.0f;
+    }
+    // ---- light sampling tree: the light mesh's own BVH (BVH::Sampling_from_root)
+    out.hdr.light_mesh = light;
+    if (light >= 0) {
+        const auto& mn = mesh_nodes[light];
+        std::vector<int> order;   // pre-order, root first
+        std::function<int(int)> lw = [&](int ni) -> int {
+            const int me = (int)order.size();
+            order.push_back(ni);
+            if (mn[ni].left >= 0) { lw(mn[ni].left); lw(mn[ni].right); }
+            return me;
+        };
+        lw(mesh_root[light]);
+        std::vector<int> pos(mn.size(), -1);
+        for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (int)k;
+        out.lnodes.resize(order.size() * 4);
+        std::vector<int> ltri_of;
+        for (size_t k = 0; k < order.size(); ++k) {
+            const BNode& b = mn[order[k]];
+            float* q = &out.lnodes[4 * k];
+            q[0] = b.area;
+            if (b.left >= 0) { q[1] = bits_as_float(pos[b.left]); q[2] = bits_as_float(pos[b.right]); q[3] = bits_as_float(-1); }
+            else { q[1] = bits_as_float(-1); q[2] = bits_as_float(-1); q[3] = bits_as_float((int)ltri_of.size()); ltri_of.push_back(b.item); }
+        }
+        out.ltris.resize(ltri_of.size() * 16);
+        for (size_t k = 0; k < ltri_of.size(); ++k) {
+            const Tri& t = tris[light][ltri_of[k]];
+            float* q = &out.ltris[16 * k];
+            q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = 0;
+            q[4] = t.b.x; q[5] = t.b.y; q[6] = t.b.z; q[7] = 0;
+            q[8] = t.c.x; q[9] = t.c.y; q[10] = t.c.z; q[11] = 0;
+            q[12] = t.n.x; q[13] = t.n.y; q[14] = t.n.z; q[15] = t.area;
+        }
+        out.hdr.light_area = mn[mesh_root[light]].area;
+        const MaterialDesc& m = meshes_[light].material;
+        out.hdr.light_emission[0] = m.emission.x; out.hdr.light_emission[1] = m.emission.y; out.hdr.light_emission[2] = m.emission.z;
+    }
+    uint32_t depth = 0;
+    {
+        std::vector<uint32_t> lv(NN, 0);
+        for (uint32_t i = 0; i < NN; ++i) {
+            if (fn[i].left >= 0) { lv[fn[i].left] = lv[i] + 1; lv[fn[i].right] = lv[i] + 1; }
+            depth = std::max(depth, lv[i]);
+        }
+    }
+    out.hdr.n_nodes = NN; out.hdr.n_tris = NT; out.hdr.n_mats = (uint32_t)nm;
+    out.hdr.n_lnodes = (uint32_t)(out.lnodes.size() / 4); out.hdr.n_ltris = (uint32_t)(out.ltris.size() / 16);
+    out.hdr.max_depth = depth;
+    return true;
+}
+
+}  // namespace rt

@@ -1,0 +1,137 @@
+/* rt_capi.h -- C-ABI of the MI355X path tracer (librt_hip.so).
+ *
+ * The drop-in boundary: the reference has no FFI; its hot path is the C++ call
+ * Renderer::Render(const Camera&) (Monte Carlo Path Tracer/8599RayTracerGUI/src/Renderer.cpp:91-122)
+ * driven by the Walnut layer (mainloop.cpp:139-148).  The C++20 host classes in include/rt/
+ * (Renderer, Camera) keep that API and call the entry points below; other hosts (ctypes, cgo,
+ * JNI) bind them directly.  Plain pointers and sizes only; no HIP/torch types;
+ * integer status codes, no exceptions across the ABI; message via rt_last_error().
+ *
+ * Reference anchors, per entry point ("MC/" = Monte Carlo Path Tracer/8599RayTracerGUI/src/):
+ *   rt_scene_add_obj / rt_scene_add_mesh  Whitted::TriangleMesh ctor + Renderer::Add        MC/TriangleMesh.h:148-186, MC/Renderer.h:78-81
+ *   rt_scene_add_cornell_box              Renderer::Renderer() scene                        MC/Renderer.cpp:26-57
+ *   rt_scene_build                        Renderer::GenerateBVH / BVH::build_BVH            MC/Renderer.h:83-86, MC/BVH.h:131-214
+ *   rt_camera_default                     Camera(35,0.1,100) + ResizeViewport matrices      MC/Camera.cpp:87-112, MC/mainloop.cpp:22
+ *   rt_resize                             Renderer::ResizeViewport                          MC/Renderer.cpp:59-89
+ *   rt_render                             Renderer::Render x n_frames (+ RayGen_Shader)     MC/Renderer.cpp:91-134
+ *   rt_reset_accumulation                 Renderer::Reaccumulate                            MC/Renderer.h:57-60
+ *   rt_trace                              Renderer::ray_BVH_intersection_record             MC/Renderer.h:88-91
+ */
+#ifndef RT_CAPI_H
+#define RT_CAPI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_API_VERSION 1
+
+typedef int32_t rt_status;
+#define RT_OK 0
+#define RT_ERR_INVALID (-1) /* bad argument / shape */
+#define RT_ERR_HIP (-2)     /* a HIP runtime call failed (message has the hipError_t name) */
+#define RT_ERR_IO (-3)      /* file not found / unparsable OBJ */
+#define RT_ERR_STATE (-4)   /* call order (no scene uploaded, no viewport) */
+#define RT_ERR_OOM (-5)     /* device allocation failed */
+
+typedef struct rt_scene rt_scene; /* host-side scene builder */
+typedef struct rt_ctx rt_ctx;     /* one device context (one GPU, one stream) */
+
+/* ------------------------------------------------------------------ scene (host) */
+rt_status rt_scene_create(rt_scene** out);
+void rt_scene_destroy(rt_scene* s);
+/* Cornell box of Renderer::Renderer(): floor, shortbox, tallbox (white), left (red), right (green), light */
+rt_status rt_scene_add_cornell_box(rt_scene* s);
+/* a TriangleMesh from an OBJ file (single mesh; positions scaled by 0.01 like the reference) */
+rt_status rt_scene_add_obj(rt_scene* s, const char* path, const float albedo[3], const float emission[3], int32_t* mesh_id);
+/* a TriangleMesh from de-indexed raw positions (9 floats per triangle, pre-scale, objl order) */
+rt_status rt_scene_add_mesh(rt_scene* s, const float* raw_positions, uint64_t n_tris, const float albedo[3], const float emission[3],
+                            int32_t* mesh_id);
+rt_status rt_scene_build(rt_scene* s);
+
+typedef struct {
+    uint32_t n_meshes, n_tris, n_nodes, n_light_tris, max_depth;
+    int32_t light_mesh;
+    float light_area;
+    uint64_t device_bytes; /* bytes the flattened scene occupies in HBM */
+} rt_scene_info;
+rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
+/* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node
+ * (left right tri mesh top_level), tri_f 13/tri (a b c n area), tri_i 2/tri (mesh material) */
+rt_status rt_scene_export(const rt_scene* s, float* node_f, int32_t* node_i, float* tri_f, int32_t* tri_i);
+
+/* ------------------------------------------------------------------ camera (host math) */
+typedef struct {
+    float position[3];
+    float inv_projection[16]; /* column-major glm::mat4 */
+    float inv_view[16];
+} rt_camera;
+/* the reference Camera (defaults MC/Camera.h:19-37, fov 35 deg, near 0.1, far 100) for a viewport;
+ * optional proj/view (16 floats each, may be NULL) */
+rt_status rt_camera_default(uint32_t width, uint32_t height, rt_camera* out, float* proj, float* view);
+/* a camera at `position` looking along `forward` (up = +y), glm::lookAt / perspectiveFov */
+rt_status rt_camera_look(uint32_t width, uint32_t height, const float position[3], const float forward[3], float vfov_deg,
+                         float near_clip, float far_clip, rt_camera* out);
+
+/* ------------------------------------------------------------------ device context */
+typedef struct {
+    int32_t device;  /* HIP device ordinal */
+    void* stream;    /* hipStream_t to launch on (NULL: the context creates its own) */
+    uint32_t flags;  /* reserved, 0 */
+} rt_device_cfg;
+rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg);
+void rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+rt_status rt_upload_scene(rt_ctx* ctx, const rt_scene* s);
+/* full image size; allocates the accumulation (float4) and RGBA8 buffers for this device's pixels.
+ * Pixels are dealt in row bands of `band` rows round-robin over `nranks` (band=8, rank=0, nranks=1
+ * for one GPU); rt_local_rows() returns how many rows this device owns. */
+rt_status rt_resize(rt_ctx* ctx, uint32_t width, uint32_t height, uint32_t band, uint32_t rank, uint32_t nranks);
+uint32_t rt_local_rows(const rt_ctx* ctx);
+
+#define RT_RENDER_EXACT 1u /* fold the recursion inner-first (bit-faithful accumulation); else forward */
+#define RT_RENDER_COUNT 2u /* collect node/triangle/ray counters (rt_get_stats) */
+typedef struct {
+    uint32_t first_frame; /* 1-based frame index of the first sample (== reference frame_accumulating) */
+    uint32_t n_frames;    /* samples per pixel rendered by this call */
+    uint64_t seed;        /* RNG key */
+    float rr;             /* Russian-roulette survival probability (MC/Renderer.h:199) */
+    uint32_t flags;       /* RT_RENDER_* */
+} rt_render_params;
+/* Renders n_frames frames into the device accumulation buffer (reset when first_frame == 1) and
+ * packs RGBA8.  Asynchronous on the context stream unless a host output pointer is given:
+ * out_rgba (local rows x width u32, ABGR, may be NULL) / out_accum (local rows x width x 4 f32,
+ * may be NULL) are filled after a stream synchronisation.  Local row r is global row
+ * (rank + (r / band) * nranks) * band + r % band. */
+rt_status rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint32_t* out_rgba, float* out_accum);
+/* device pointers of the local accumulation (float4) and RGBA8 buffers */
+rt_status rt_device_buffers(rt_ctx* ctx, void** d_accum, void** d_rgba);
+/* copy device RGBA8 to a caller device pointer (e.g. a torch tensor) on the context stream */
+rt_status rt_copy_rgba_to_device(rt_ctx* ctx, void* dst);
+rt_status rt_reset_accumulation(rt_ctx* ctx);
+rt_status rt_synchronize(rt_ctx* ctx);
+
+typedef struct {
+    float last_kernel_ms;     /* megakernel duration of the last rt_render (HIP events, same stream) */
+    uint64_t node_tests;      /* RT_RENDER_COUNT only */
+    uint64_t tri_tests;
+    uint64_t rays;
+    uint64_t stack_overflows; /* paths deeper than the EXACT fold stack (expected 0) */
+    uint64_t samples;
+    uint32_t grid, block, stack_depth;
+} rt_stats;
+rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
+
+/* closest hit of n rays (host arrays; tri = flattened triangle slot or -1, t = double distance) */
+rt_status rt_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t);
+/* device arithmetic self-test: for each x: sqrtf, 1/x, cos, sin (as the kernel evaluates them),
+ * and the double reciprocal's low/high words -> 6 floats per input */
+rt_status rt_math_selftest(rt_ctx* ctx, uint64_t n, const float* x, float* out);
+
+int32_t rt_api_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,137 @@
+"""C-ABI checks that need no GPU: the library loads and exports every declared entry point; the
+host scene path (built-in Cornell box, OBJ loader, reference-identical BVH build + flattening) and
+the camera matrices are bit-identical to the reference's (golden fixtures)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _rt import REPO, rt
+
+G = O.GOLDEN
+MESH_MATERIAL = np.array([2, 2, 2, 0, 1, 3])
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64 if a.dtype == np.float64 else a.dtype)
+
+
+def declared_functions():
+    names = set()
+    for h in ("include/rt_capi.h",):
+        txt = open(os.path.join(REPO, h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        names |= set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", txt))
+    return sorted(names)
+
+
+def test_library_exports_every_declared_symbol():
+    L = rt.lib()
+    names = declared_functions()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    assert L.rt_api_version() == 1
+
+
+def golden_scene():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gg", os.path.join(O.ORACLE_DIR, "gen_golden.py"))
+    gg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gg)
+    z = np.load(os.path.join(G, "cornell_scene.npz"))
+    return z["nodes"].view(gg.NODE_DT), z["tris"].view(gg.TRI_DT)
+
+
+def check_scene(scene):
+    nodes, tris = golden_scene()
+    nf, ni, tf, ti = scene.export()
+    assert nf.shape[0] == len(nodes) and tf.shape[0] == len(tris)
+    assert np.array_equal(bits(nf[:, 0:3]), bits(nodes["mn"]))
+    assert np.array_equal(bits(nf[:, 3:6]), bits(nodes["mx"]))
+    assert np.array_equal(bits(nf[:, 6]), bits(nodes["area"]))
+    for k, col in (("left", 0), ("right", 1), ("tri", 2), ("mesh", 3), ("top", 4)):
+        assert np.array_equal(ni[:, col], nodes[k]), k
+    for k, sl in (("a", slice(0, 3)), ("b", slice(3, 6)), ("c", slice(6, 9)), ("n", slice(9, 12))):
+        assert np.array_equal(bits(tf[:, sl]), bits(tris[k])), k
+    assert np.array_equal(bits(tf[:, 12]), bits(tris["area"]))
+    assert np.array_equal(ti[:, 0], tris["mesh"])
+    assert np.array_equal(MESH_MATERIAL[ti[:, 1]], tris["material"])
+
+
+def test_builtin_cornell_box_equals_reference_scene():
+    s = rt.Scene.cornell()
+    check_scene(s)
+    info = s.info()
+    assert info.n_tris == 32 and info.n_nodes == 63 and info.light_mesh == 5 and info.n_light_tris == 2
+    assert np.float32(info.light_area) == np.float32(1.3649999)
+
+
+def test_scene_from_raw_meshes_equals_reference_scene():
+    s = rt.Scene()
+    for (_, raw, alb, em) in O.cornell_meshes():
+        s.add_mesh(raw, alb, em)
+    s.build()
+    check_scene(s)
+
+
+def test_obj_loader_equals_reference_loader(tmp_path):
+    ref = "/root/reference/Monte Carlo Path Tracer/8599RayTracerGUI/src/cornellbox"
+    meshes = O.cornell_meshes()
+    s = rt.Scene()
+    for (name, raw, alb, em) in meshes:
+        path = os.path.join(ref, name + ".obj")
+        if not os.path.exists(path):
+            # GPU box: no reference tree -- write the fixture positions as an OBJ (same numbers)
+            path = str(tmp_path / (name + ".obj"))
+            with open(path, "w") as f:
+                for v in raw.reshape(-1, 3):
+                    f.write("v %r %r %r\n" % tuple(float(c) for c in v))
+                for i in range(raw.shape[0]):
+                    f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+        s.add_obj(path, alb, em)
+    s.build()
+    check_scene(s)
+
+
+def test_obj_loader_edge_cases(tmp_path):
+    p = tmp_path / "q.obj"
+    p.write_text("# c\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvn 0 0 1\nf 1//1 2//1 3//1\nf -4 -2 -1\n")
+    s = rt.Scene()
+    s.add_obj(str(p), [0.5, 0.5, 0.5], [0, 0, 0])
+    s.add_obj(str(p), [0.5, 0.5, 0.5], [1, 1, 1])
+    s.build()
+    nf, ni, tf, ti = s.export()
+    assert tf.shape[0] == 4
+    with pytest.raises(rt.RtError):
+        rt.Scene().add_obj(str(tmp_path / "missing.obj"), [1, 1, 1], [0, 0, 0])
+    with pytest.raises(rt.RtError):
+        rt.Scene().build()   # empty scene
+
+
+def test_camera_matrices_equal_reference():
+    z = np.load(os.path.join(G, "camera.npz"))
+    n = 0
+    for key in z.files:
+        if key.startswith("mats_") and "_f" not in key:
+            W, H = map(int, key[5:].split("x"))
+            cam, proj, view = rt.camera_default(W, H)
+            g = z[key]
+            assert np.array_equal(bits(proj), bits(g[0].ravel())), key
+            assert np.array_equal(bits(np.array(cam.inv_projection, np.float32)), bits(g[1].ravel())), key
+            assert np.array_equal(bits(view), bits(g[2].ravel())), key
+            assert np.array_equal(bits(np.array(cam.inv_view, np.float32)), bits(g[3].ravel())), key
+            assert np.array_equal(bits(np.array(cam.position, np.float32)), bits(z["vec_16x16_f1_s0"][:3]))
+            n += 1
+    assert n == 8
+
+
+def test_context_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(rt.RtError):
+        rt.Context(0)

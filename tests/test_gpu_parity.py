@@ -1,0 +1,125 @@
+"""GPU parity: the HIP megakernel (through the C-ABI) against the reference's golden vectors and the
+oracle.  Tolerance (north star): per-pixel RMSE < 1e-4 of clamp(accum/spp, 0, 1) at matched spp.
+The accumulation is expected to be bitwise identical except where a 1-ulp difference between
+glibc's cosf/sinf and the kernel's correctly rounded cos/sin changes a path."""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _rt import rt
+
+pytestmark = pytest.mark.gpu
+G = O.GOLDEN
+RMSE_TOL = 1e-4
+
+
+def bits(a):
+    a = np.ascontiguousarray(a)
+    return a.view(np.uint32 if a.dtype == np.float32 else np.uint64 if a.dtype == np.float64 else a.dtype)
+
+
+def rmse(acc, ref, spp):
+    a = np.clip(acc[..., :3] / np.float32(spp), 0, 1).astype(np.float64)
+    b = np.clip(ref[..., :3] / np.float32(spp), 0, 1).astype(np.float64)
+    return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = rt.Context(0)
+    c.upload(rt.Scene.cornell())
+    yield c
+    c.close()
+
+
+def render(ctx, W, H, spp, seed=0, rr=0.8, exact=True, band=8, rank=0, nranks=1, first_frame=1):
+    ctx.resize(W, H, band, rank, nranks)
+    cam, _, _ = rt.camera_default(W, H)
+    return ctx.render(cam, spp, first_frame=first_frame, seed=seed, rr=rr, exact=exact)
+
+
+def test_device_arithmetic_is_ieee(ctx):
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.uniform(0, 7, 200000), rng.uniform(1e-6, 1e6, 200000), [0.5, 1.0, 2.0, 6.2831855]]).astype(np.float32)
+    out = ctx.math_selftest(x)
+    assert np.array_equal(bits(out[:, 0]), bits(np.sqrt(x)))                        # correctly rounded sqrtf
+    assert np.array_equal(bits(out[:, 1]), bits(np.float32(1.0) / x))                # correctly rounded f32 division
+    r = out[:, 4:6].copy().view(np.float64).ravel()
+    assert np.array_equal(bits(r), bits(1.0 / x.astype(np.float64)))                 # f64 reciprocal
+    cr_cos = np.cos(x.astype(np.float64)).astype(np.float32)
+    assert np.mean(out[:, 2] == cr_cos) > 0.999999                                   # correctly rounded cos
+    assert np.max(np.abs(out[:, 3] - np.sin(x.astype(np.float64)))) < 1e-6
+
+
+def test_closest_hit_matches_reference(ctx):
+    z = np.load(os.path.join(G, "rays_cornell.npz"))
+    tri, t = ctx.trace(z["org"], z["dir"])
+    assert np.array_equal(tri, z["tri"])
+    hit = z["hit"] == 1
+    assert np.array_equal(bits(t[hit]), bits(z["t"][hit]))
+
+
+@pytest.mark.parametrize("key", ["64x64_spp1_s0_rr0.8", "64x64_spp16_s0_rr0.8", "64x64_spp256_s0_rr0.8",
+                                 "128x128_spp16_s7_rr0.8", "40x30_spp8_s123_rr0.5", "33x17_spp4_s5_rr0.9"])
+def test_image_matches_reference_golden(ctx, key):
+    z = np.load(os.path.join(G, "images_cornell.npz"))
+    wh, spp, s, rr = key.split("_")
+    W, H = map(int, wh.split("x"))
+    spp = int(spp[3:])
+    rgba, acc = render(ctx, W, H, spp, seed=int(s[1:]), rr=float(rr[2:]))
+    g_acc, g_rgba = z[f"accum_{key}"], z[f"rgba_{key}"]
+    e = rmse(acc, g_acc, spp)
+    same = np.mean(np.all(bits(acc) == bits(g_acc), axis=-1))
+    d8 = np.abs(rgba.view(np.uint8).astype(int) - g_rgba.view(np.uint8).astype(int)).max()
+    print(f"{key}: rmse {e:.3e} bitwise-identical pixels {same:.4%} max |d8| {d8}")
+    assert e < RMSE_TOL
+    assert same > 0.97
+
+
+def test_fast_mode_within_tolerance(ctx):
+    _, a = render(ctx, 64, 64, 64, exact=True)
+    _, b = render(ctx, 64, 64, 64, exact=False)
+    assert rmse(a, b, 64) < 1e-5
+
+
+def test_incremental_frames_equal_batched(ctx):
+    _, a = render(ctx, 48, 40, 5, seed=11)
+    ctx.resize(48, 40)
+    cam, _, _ = rt.camera_default(48, 40)
+    for f in range(1, 6):
+        rgba, acc = ctx.render(cam, 1, first_frame=f, seed=11)
+    assert np.array_equal(bits(acc), bits(a))
+
+
+def test_row_band_split_reassembles_bitwise(ctx):
+    W, H, spp = 70, 45, 4
+    rgba1, acc1 = render(ctx, W, H, spp, seed=3)
+    full = np.zeros_like(acc1)
+    for r in range(3):
+        rgba, acc = render(ctx, W, H, spp, seed=3, band=8, rank=r, nranks=3)
+        rows = ctx.local_to_global_rows()
+        full[rows] = acc
+    assert np.array_equal(bits(full), bits(acc1))
+
+
+def test_matches_oracle_at_larger_size(ctx):
+    W, H, spp = 192, 160, 32
+    rgba, acc = render(ctx, W, H, spp, seed=5)
+    sc = O.Scene()
+    oacc, orgba, _ = sc.render(W, H, spp, seed=5)
+    e = rmse(acc, oacc, spp)
+    same = np.mean(np.all(bits(acc) == bits(oacc), axis=-1))
+    print(f"oracle {W}x{H}x{spp}: rmse {e:.3e} identical {same:.4%}")
+    assert e < RMSE_TOL and same > 0.97
+
+
+def test_counters_and_no_stack_overflow(ctx):
+    ctx.resize(64, 64)
+    cam, _, _ = rt.camera_default(64, 64)
+    ctx.render(cam, 16, exact=True, count=True, fetch=False)
+    st = ctx.stats()
+    assert st.samples == 64 * 64 * 16 and st.stack_overflows == 0
+    assert 4.0 < st.rays / st.samples < 7.5
+    assert st.node_tests > st.rays and st.tri_tests > 0 and st.last_kernel_ms > 0
