@@ -3,9 +3,8 @@
 // Every expression mirrors the reference (MC/ = "Monte Carlo Path Tracer/8599RayTracerGUI/src/")
 // and glm 0.9.9.9 (GLM/ = ".../Walnut/vendor/glm/glm/") term by term.  The file is compiled with
 // -ffp-contract=off, without fast-math, and with correctly rounded f32 division/sqrt, so each
-// operation is the same IEEE operation the CPU reference performs.  Transcendentals (cos/sin of the
-// hemisphere angle) are evaluated in double and rounded once (correctly rounded f32 results);
-// glibc's cosf/sinf differ from that in ~0.05-0.1 % of arguments by one ulp ("Parity").
+// operation is the same IEEE operation the CPU reference performs.  cos/sin of the hemisphere
+// angle restate glibc's cosf/sinf (what the reference calls on Linux) bit for bit on [0, 2*PI].
 #ifndef RT_DEVICE_H
 #define RT_DEVICE_H
 #include <hip/hip_runtime.h>
@@ -138,9 +137,75 @@ __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const
     return (t > 0.0) && (b2 > 0.0) && (b3 > 0.0) && (((1.0 - b2) - b3) > 0.0);
 }
 
-// cos/sin of the hemisphere angle: double evaluation, one rounding (see header)
-__device__ __forceinline__ float cos_f(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float sin_f(float x) { return (float)sin((double)x); }
+// cos/sin of the hemisphere angle phi = 2*PI*U in [0, 2*PI] (MC/WhittedMaterial.h:80-81 calls
+// std::cos/std::sin(float) -> glibc cosf/sinf).  Restatement of glibc 2.35's single-precision
+// algorithm (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h; ARM optimized-routines):
+// double-precision Cody-Waite style reduction by pi/2 (`reduce_fast`, 0 <= x < 120) and two
+// polynomials, one rounding to float.  Verified bit-identical to glibc's sinf/cosf for every float
+// in [0, 2*PI] (both its FMA and non-FMA builds), see tests/test_device_trig.py.
+namespace glibc_trig {
+constexpr double S1 = -0x1.555545995a603p-3, S2 = 0x1.1107605230bc4p-7, S3 = -0x1.994eb3774cf24p-13;
+constexpr double C0 = 0x1p0, C1 = -0x1.ffffffd0c621cp-2, C2 = 0x1.55553e1068f19p-5, C3 = -0x1.6c087e89a359dp-10,
+                 C4 = 0x1.99343027bf8c3p-16;
+constexpr double HPI_INV = 0x1.45F306DC9C883p+23, HPI = 0x1.921FB54442D18p0;
+__device__ __forceinline__ uint32_t top12(float x) { return ((uint32_t)__float_as_int(x) >> 20) & 0x7ffu; }
+// sinf_poly: odd n -> cosine polynomial, even n -> sine polynomial
+__device__ __forceinline__ double poly(double x, double x2, int n)
+{
+    if ((n & 1) == 0) {
+        const double x3 = x * x2;
+        const double s1 = S2 + x2 * S3;
+        const double x7 = x3 * x2;
+        const double s = x + x3 * S1;
+        return s + x7 * s1;
+    }
+    const double x4 = x2 * x2;
+    const double c2 = C3 + x2 * C4;
+    const double c1 = C0 + x2 * C1;
+    const double x6 = x4 * x2;
+    const double c = c1 + x4 * C2;
+    return c + x6 * c2;
+}
+// x in [0, 120): quadrant n and reduced argument (reduce_fast)
+__device__ __forceinline__ double reduce(double x, int& n)
+{
+    const double r = x * HPI_INV;
+    n = ((int32_t)r + 0x800000) >> 24;
+    return x - (double)n * HPI;
+}
+}  // namespace glibc_trig
+
+__device__ __forceinline__ float cos_f(float y)
+{
+    using namespace glibc_trig;
+    double x = y;
+    if (top12(y) < top12(0x1.921FB6p-1f)) {   // |y| < pi/4
+        if (top12(y) < top12(0x1p-12f)) return 1.0f;
+        return (float)poly(x, x * x, 1);
+    }
+    int n;
+    x = reduce(x, n);
+    const double s = (n & 2) ? ((n & 1) ? 1.0 : -1.0) : ((n & 1) ? -1.0 : 1.0);   // sign[n & 3] = {1,-1,-1,1}
+    double r = poly(x * s, x * x, n ^ 1);
+    if (((n ^ 1) & 1) && (n & 2)) r = -r;   // second table: negated cosine coefficients
+    return (float)r;
+}
+
+__device__ __forceinline__ float sin_f(float y)
+{
+    using namespace glibc_trig;
+    double x = y;
+    if (top12(y) < top12(0x1.921FB6p-1f)) {
+        if (top12(y) < top12(0x1p-12f)) return y;
+        return (float)poly(x, x * x, 0);
+    }
+    int n;
+    x = reduce(x, n);
+    const double s = (n & 2) ? ((n & 1) ? 1.0 : -1.0) : ((n & 1) ? -1.0 : 1.0);
+    double r = poly(x * s, x * x, n);
+    if ((n & 1) && (n & 2)) r = -r;
+    return (float)r;
+}
 
 // glm mat4 * vec4, GLM/detail/type_mat4x4.inl:561-572: (m0*v0 + m1*v1) + (m2*v2 + m3*v3); m column-major
 __device__ __forceinline__ void mat4_mul(const float* m, float v0, float v1, float v2, float v3, float out[4])

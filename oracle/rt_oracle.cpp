@@ -770,6 +770,11 @@ void or_material_sample(int64_t n, const float* nrm, const float* wi, const uint
     }
 }
 
+void or_trig(int64_t n, const float* x, float* cos_out, float* sin_out)
+{   // the libm the reference calls (std::cos/std::sin on float, MC/WhittedMaterial.h:80-81)
+    for (int64_t i = 0; i < n; ++i) { cos_out[i] = cosf(x[i]); sin_out[i] = sinf(x[i]); }
+}
+
 uint32_t or_rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim) { return oracle_rng_u32(seed, pixel, frame, dim); }
 float or_rng_float(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim) { return oracle_u32_to_float(oracle_rng_u32(seed, pixel, frame, dim)); }
 

@@ -73,6 +73,9 @@ void or_light_sample(const or_scene* s, int64_t n, const uint32_t* u, float* loc
 void or_material_sample(int64_t n, const float* nrm, const float* wi, const uint32_t* u, const float* albedo,
                         float* raw, float* dir, float* brdf, float* pdf);
 
+/* libm cosf/sinf of n floats */
+void or_trig(int64_t n, const float* x, float* cos_out, float* sin_out);
+
 /* the RNG stream itself (oracle/philox.h) */
 uint32_t or_rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim);
 float or_rng_float(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim);

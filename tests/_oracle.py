@@ -57,6 +57,7 @@ def lib():
                                       C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.or_material_sample.argtypes = [C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                          C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.or_trig.argtypes = [C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         _lib = L
     return _lib
 
@@ -166,3 +167,10 @@ def material_sample(n, wi, u, albedo):
     lib().or_material_sample(k, _p(n, C.c_float), _p(wi, C.c_float), _p(u, C.c_uint32), _p(albedo, C.c_float),
                              _p(raw, C.c_float), _p(d, C.c_float), _p(b, C.c_float), _p(pdf, C.c_float))
     return raw, d, b, pdf
+
+
+def libm_trig(x):
+    x = np.ascontiguousarray(x, np.float32)
+    c = np.zeros_like(x); s = np.zeros_like(x)
+    lib().or_trig(x.shape[0], _p(x, C.c_float), _p(c, C.c_float), _p(s, C.c_float))
+    return c, s
