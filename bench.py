@@ -122,7 +122,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream shared by the megakernel, the copies, RCCL and the torch ops,
+    # so every step is ordered on ONE stream and torch.cuda.Event sees the kernel
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    assert stream.cuda_stream != 0
 
     rt = load_pkg()
     W, H, spp = args.width, args.height, args.spp

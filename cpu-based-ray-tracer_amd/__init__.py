@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 RT_OK = 0
 RENDER_EXACT = 1
 RENDER_COUNT = 2
+RENDER_GLOBAL_SCENE = 4
+RENDER_GLOBAL_STACK = 8
 
 _lib = None
 
@@ -194,8 +196,11 @@ class Context:
         self.band, self.rank, self.nranks = band, rank, nranks
         self.local_rows = lib().rt_local_rows(self.h)
 
-    def render(self, cam, n_frames, first_frame=1, seed=0, rr=0.8, exact=True, count=False, fetch=True):
-        p = RenderParams(first_frame, n_frames, seed, rr, (RENDER_EXACT if exact else 0) | (RENDER_COUNT if count else 0))
+    def render(self, cam, n_frames, first_frame=1, seed=0, rr=0.8, exact=True, count=False, fetch=True, global_scene=False,
+               global_stack=False):
+        flags = (RENDER_EXACT if exact else 0) | (RENDER_COUNT if count else 0) | (RENDER_GLOBAL_SCENE if global_scene else 0)
+        flags |= RENDER_GLOBAL_STACK if global_stack else 0
+        p = RenderParams(first_frame, n_frames, seed, rr, flags)
         if fetch:
             rgba = np.zeros((self.local_rows, self.W), np.uint32)
             acc = np.zeros((self.local_rows, self.W, 4), np.float32)

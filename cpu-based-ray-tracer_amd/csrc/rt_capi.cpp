@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -40,15 +41,17 @@ struct rt_ctx {
     uint32_t stack_depth = 0;
     uint32_t grid = 0, block = 256, total_threads = 0;   // grid of the EXACT kernel (sizes the fold stack)
     uint32_t n_cu = 0;
-    int occ[2][2] = {{0, 0}, {0, 0}};                     // blocks per CU, [exact][count]
+    int occ_global[2][2] = {{0, 0}, {0, 0}};              // blocks per CU, [exact][count], scene in HBM
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     rt_stats stats{};
     bool pending_stats = false;
     uint32_t last_flags = 0;
+    uint32_t thresh = 8, steps = 8;    // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
 
 namespace {
 
+constexpr size_t kMaxLdsScene = 48 * 1024;   // scenes up to ~700 triangles live in LDS
 constexpr uint32_t kStackDepth = 192;   // EXACT fold stack; RR 0.8 => P(depth > 192) ~ 2.5e-19 per sample
 
 rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what)
@@ -173,6 +176,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     rt_ctx* c = new (std::nothrow) rt_ctx;
     if (!c) return RT_ERR_OOM;
     c->device = cfg ? cfg->device : 0;
+    if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
     if (cfg && cfg->stream) {
@@ -198,11 +203,13 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     int ex_max = 1;
     for (int ex = 0; ex < 2; ++ex)
         for (int cn = 0; cn < 2; ++cn) {
-            int b = rt_megakernel_occupancy(ex, cn, 256);
-            c->occ[ex][cn] = b > 0 ? b : 2;
-            if (ex) ex_max = std::max(ex_max, c->occ[ex][cn]);
+            int b = rt_megakernel_occupancy(ex, cn, false, 256, 0);
+            c->occ_global[ex][cn] = b > 0 ? b : 2;
+            if (ex) ex_max = std::max(ex_max, c->occ_global[ex][cn]);
         }
     c->block = 256;
+    // the EXACT fold stack is sized for the largest grid any mode launches (LDS staging never
+    // raises occupancy above the register-limited value)
     c->grid = c->n_cu * (uint32_t)ex_max;
     c->total_threads = c->grid * c->block;
     *out = c;
@@ -279,7 +286,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     }
     KParams P{};
     P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes;
-    P.tris = c->d_tris; P.mats = c->d_mats; P.lnodes = c->d_lnodes; P.ltris = c->d_ltris;
+    P.tris = c->d_tris; P.n_tris = c->hdr.n_tris;
+    P.mats = c->d_mats; P.n_mats = c->hdr.n_mats;
+    P.lnodes = c->d_lnodes; P.n_lnodes = c->hdr.n_lnodes;
+    P.ltris = c->d_ltris; P.n_ltris = c->hdr.n_ltris;
     P.light_area = c->hdr.light_area;
     std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
     P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;
@@ -299,13 +309,30 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
-    const uint32_t grid = exact ? c->grid : c->n_cu * (uint32_t)c->occ[0][count ? 1 : 0];
+    P.thresh = c->thresh; P.steps = c->steps;
+    // small scenes are staged into LDS (one copy per workgroup)
+    const size_t lds_bytes = rt_scene_lds_bytes(P);
+    const bool lds = (p->flags & RT_RENDER_GLOBAL_SCENE) == 0 && lds_bytes <= kMaxLdsScene;
+    P.lds_scene_quads = lds ? (uint32_t)(lds_bytes / sizeof(float4)) : 0;
+    // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
+    // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
+    P.lds_levels = 0;
+    if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
+        const size_t budget = 40 * 1024, used = lds ? lds_bytes : 0;
+        for (uint32_t lv = 8; lv > 0; --lv)
+            if (used + rt_stack_lds_bytes(lv) <= budget) { P.lds_levels = lv; break; }
+    }
+    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
+    int bpc = rt_megakernel_occupancy(exact, count, lds, (int)c->block, shmem);
+    if (bpc <= 0) bpc = c->occ_global[exact][count];
+    uint32_t grid = c->n_cu * (uint32_t)bpc;
+    if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
     HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
     HIPC(c, hipMemsetAsync(c->d_counters, 0, 64, c->stream));
     c->last_flags = p->flags;
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
-        HIPC(c, rt_launch_megakernel(P, exact, count, grid, c->block, c->stream));
+        HIPC(c, rt_launch_megakernel(P, exact, count, lds, grid, c->block, c->stream));
         c->stats.grid = grid;
         HIPC(c, hipEventRecord(c->ev1, c->stream));
         c->pending_stats = true;

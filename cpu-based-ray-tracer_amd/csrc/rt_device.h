@@ -115,6 +115,26 @@ __device__ __forceinline__ bool slab_hit(const Ray& r, float lx, float ly, float
     return (tout >= 0.0f) && (tin <= tout);
 }
 
+// The same test without NaN semantics, for rays whose reciprocal direction is finite in every
+// component: then no (slab - o) * rcp is NaN (0 * inf needs an infinite reciprocal), and IEEE
+// max/min agree with std::max/std::min up to the sign of a zero, which the two comparisons below do
+// not see.  Lowers to v_max3_f32 / v_min3_f32.
+__device__ __forceinline__ bool slab_hit_finite(const Ray& r, float lx, float ly, float lz, float hx, float hy, float hz)
+{
+    const float ax = r.nx ? hx : lx, bx = r.nx ? lx : hx;
+    const float ay = r.ny ? hy : ly, by = r.ny ? ly : hy;
+    const float az = r.nz ? hz : lz, bz = r.nz ? lz : hz;
+    const float tix = (ax - r.o.x) * r.rcp.x, tiy = (ay - r.o.y) * r.rcp.y, tiz = (az - r.o.z) * r.rcp.z;
+    const float tox = (bx - r.o.x) * r.rcp.x, toy = (by - r.o.y) * r.rcp.y, toz = (bz - r.o.z) * r.rcp.z;
+    const float tin = __builtin_fmaxf(tix, __builtin_fmaxf(tiy, tiz));
+    const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
+    return (tout >= 0.0f) && (tin <= tout);
+}
+__device__ __forceinline__ bool rcp_finite(const Ray& r)
+{
+    return __builtin_isfinite(r.rcp.x) && __builtin_isfinite(r.rcp.y) && __builtin_isfinite(r.rcp.z);
+}
+
 // Whitted::RayTriangleIntersection, MC/TriangleMesh.h:19-45 (float cross/dot, double reciprocal
 // and barycentrics, strict inequalities).  A float sign pre-test rejects exactly the cases whose
 // double products cannot all be positive; a conservative |b2+b3| > |den| screen rejects cases the

@@ -7,10 +7,10 @@
 struct KParams {
     // scene (rt_layout.h)
     const float4* nodes; uint32_t n_nodes;
-    const float4* tris;
-    const float4* mats;
-    const float4* lnodes;
-    const float4* ltris;
+    const float4* tris; uint32_t n_tris;
+    const float4* mats; uint32_t n_mats;
+    const float4* lnodes; uint32_t n_lnodes;
+    const float4* ltris; uint32_t n_ltris;
     float light_area; float light_emission[3]; int has_light;
     // camera: position, inverse projection, inverse view (column-major glm mat4)
     float cam_pos[3]; float iproj[16]; float iview[16];
@@ -26,12 +26,20 @@ struct KParams {
     // scratch
     uint32_t* work_counter;
     float4* stack_ld; int32_t* stack_mat; uint32_t stack_depth; uint32_t total_threads;
+    uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
+    uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
+    uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
+    uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
 };
 
-hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, uint32_t grid, uint32_t block, hipStream_t stream);
+// LDS staging of the scene: bytes needed (the kernel's dynamic shared memory when lds == true)
+size_t rt_scene_lds_bytes(const KParams& P);
+// bytes of LDS per 256-lane workgroup for `levels` EXACT stack levels (float4 + u8 material per lane)
+size_t rt_stack_lds_bytes(uint32_t levels);
+hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
+int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
-int rt_megakernel_occupancy(bool exact, bool count, int block);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);
 
 #endif

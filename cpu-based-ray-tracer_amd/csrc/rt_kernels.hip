@@ -7,18 +7,20 @@
 //   * per-pixel frames run in order inside the lane (accum += L per frame exactly like
 //     Renderer::RayGen_Shader, MC/Renderer.cpp:124-134), so the float accumulation is the
 //     reference's, bit for bit;
-//   * path regeneration: each loop iteration advances every lane by one ray segment (camera ray,
-//     or one bounce = closest hit + light sample + shadow ray + Russian roulette); a lane whose path
-//     ended starts its next frame immediately;
+//   * path regeneration + one traversal per loop iteration: every lane advances by exactly one ray
+//     (a camera/indirect closest-hit ray, or a shadow ray); shading is split at the shadow ray, so
+//     all lanes of a wave run the same traversal loop each iteration whatever phase their path is in;
 //   * the recursion of Renderer::shading (MC/Renderer.cpp:148-214) is made iterative: each bounce's
-//     (direct radiance, cosine, material) is pushed to a per-lane stack in HBM and folded back in
-//     the reference's inner-first order when the path ends (EXACT mode), or accumulated forward
+//     (direct radiance, cosine, material) is pushed to a per-lane stack and folded back in the
+//     reference's inner-first order when the path ends (EXACT mode), or accumulated forward
 //     (FAST mode: one rounding difference per bounce);
 //   * BVH traversal is stackless: nodes are in DFS pre-order with skip links (rt_layout.h), so a
 //     closest-hit walk tests exactly the boxes/triangles the reference's recursion tests
 //     (BVH::traverse_BVH_from_node, MC/BVH.h:82-101, ties to the later leaf); shadow rays are
 //     any-hit with early exit, which is exact because the reference's visibility predicate
-//     `length(q-p) < t_closest + 0.01f` (MC/Renderer.cpp:184) is monotone in t.
+//     `length(q-p) < t_closest + 0.01f` (MC/Renderer.cpp:184) is monotone in t;
+//   * small scenes (the Cornell box: 4.4 KB) are staged into LDS once per workgroup and traversed
+//     from LDS; large scenes are read through L1/L2/MALL from HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,97 +31,84 @@ using namespace rtd;
 
 namespace {
 
-
-struct Hit {
-    double t;
-    int tri;
+struct SceneView {
+    const float4* nodes;
+    const float4* tris;
+    const float4* mats;
+    const float4* lnodes;
+    const float4* ltris;
+    uint32_t n_nodes;
 };
 
-template <bool COUNT>
-__device__ __forceinline__ Hit closest_hit(const KParams& P, const Ray& r, uint32_t& node_tests, uint32_t& tri_tests)
+// One traversal: closest hit (shadow == false) or any blocking hit (shadow == true).
+// Leaf triangles are postponed: a lane that reaches a leaf whose box it hits parks the triangle and
+// the wave keeps walking boxes until every lane has a parked triangle or has finished; then all
+// parked triangles are intersected together (Aila & Laine's while-while), so the Moller-Trumbore
+// body runs once per "leaf round" instead of once per box step.  Each lane still tests its
+// triangles in DFS order, so the tie rule (later leaf wins) and the any-hit exit are unchanged.
+template <bool COUNT, bool FINITE>
+__device__ __forceinline__ void traverse_impl(const SceneView& S, const Ray& r, bool shadow, double slen, double& best, int& best_tri,
+                                              bool& occluded, uint32_t& node_tests, uint32_t& tri_tests)
 {
-    double best = 1.7976931348623157e308;   // DBL_MAX (IntersectionRecord default, MC/IntersectionRecord.h:20-28)
-    int best_tri = -1;
-    const float4* __restrict__ nodes = P.nodes;
-    const float4* __restrict__ tris = P.tris;
     uint32_t i = 0;
-    const uint32_t n = P.n_nodes;
-    while (i < n) {
-        const float4 q0 = nodes[2 * i];
-        const float4 q1 = nodes[2 * i + 1];
-        if (COUNT) ++node_tests;
-        const uint32_t skip = (uint32_t)f2i(q1.z);
-        if (slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y)) {
+    const uint32_t n = S.n_nodes;
+    for (;;) {
+        int parked = -1;
+        while (i < n) {
+            const float4 q0 = S.nodes[2 * i];
+            const float4 q1 = S.nodes[2 * i + 1];
+            if (COUNT) ++node_tests;
+            const bool hit = FINITE ? slab_hit_finite(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y)
+                                    : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
             const int tri = f2i(q1.w);
-            if (tri >= 0) {
-                if (COUNT) ++tri_tests;
-                const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
-                double t;
-                // (left.t < right.t) ? left : right  ==> the later leaf wins ties (t <= best)
-                if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t) && t <= best) {
-                    best = t; best_tri = tri;
-                }
-                i = skip;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = skip;
+            const uint32_t skip = (uint32_t)f2i(q1.z);
+            i = (hit && tri < 0) ? i + 1 : skip;
+            if (hit && tri >= 0) { parked = tri; break; }
         }
+        if (parked >= 0) {
+            if (COUNT) ++tri_tests;
+            const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
+            double t;
+            if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
+                if (shadow) {
+                    // not occluded iff length(q-p) < t + 0.01f for every hit (MC/Renderer.cpp:184)
+                    if (!(slen < t + (double)0.01f)) { occluded = true; i = n; }
+                } else if (t <= best) {
+                    // (left.t < right.t) ? left : right  ==> the later leaf wins ties
+                    best = t; best_tri = parked;
+                }
+            }
+        }
+        if (i >= n) break;
     }
-    return Hit{best, best_tri};
 }
 
-// occluded iff some hit t_i has !(len < t_i + 0.01f)  (MC/Renderer.cpp:184, evaluated in double)
 template <bool COUNT>
-__device__ __forceinline__ bool occluded(const KParams& P, const Ray& r, double len, uint32_t& node_tests, uint32_t& tri_tests)
+__device__ __forceinline__ void traverse(const SceneView& S, const Ray& r, bool shadow, double slen, double& best, int& best_tri,
+                                         bool& occluded, uint32_t& node_tests, uint32_t& tri_tests)
 {
-    const float4* __restrict__ nodes = P.nodes;
-    const float4* __restrict__ tris = P.tris;
-    uint32_t i = 0;
-    const uint32_t n = P.n_nodes;
-    while (i < n) {
-        const float4 q0 = nodes[2 * i];
-        const float4 q1 = nodes[2 * i + 1];
-        if (COUNT) ++node_tests;
-        const uint32_t skip = (uint32_t)f2i(q1.z);
-        if (slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y)) {
-            const int tri = f2i(q1.w);
-            if (tri >= 0) {
-                if (COUNT) ++tri_tests;
-                const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
-                double t;
-                if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
-                    if (!(len < t + (double)0.01f)) return true;
-                }
-                i = skip;
-            } else {
-                i = i + 1;
-            }
-        } else {
-            i = skip;
-        }
-    }
-    return false;
+    // wave-uniform choice: IEEE min/max when no lane can produce a NaN slab distance
+    if (__all(rcp_finite(r))) traverse_impl<COUNT, true>(S, r, shadow, slen, best, best_tri, occluded, node_tests, tri_tests);
+    else traverse_impl<COUNT, false>(S, r, shadow, slen, best, best_tri, occluded, node_tests, tri_tests);
 }
 
 // SamplingAreaLight -> TriangleMesh::Sampling -> BVH::Sampling_from_root/_node -> TrianglePrimitive::Sampling
 // (MC/Renderer.h:163-180, MC/TriangleMesh.h:193-197, MC/BVH.h:103-129, MC/TriangleMesh.h:69-89)
-__device__ __forceinline__ void sample_light(const KParams& P, Rng& g, V3& q, V3& nl)
+__device__ __forceinline__ void sample_light(const SceneView& S, float light_area, Rng& g, V3& q, V3& nl)
 {
     const float u0 = g.next();
-    float p = u0 * P.light_area;
+    float p = u0 * light_area;
     int node = 0;
     for (;;) {
-        const float4 ln = P.lnodes[node];
+        const float4 ln = S.lnodes[node];
         const int left = f2i(ln.y);
         if (left < 0) break;
-        const float la = P.lnodes[left].x;
+        const float la = S.lnodes[left].x;
         if (p < la) node = left;
         else { p = p - la; node = f2i(ln.z); }
     }
-    const int lt = f2i(P.lnodes[node].w);
-    const float4 A = P.ltris[4 * lt], B = P.ltris[4 * lt + 1], C = P.ltris[4 * lt + 2], N = P.ltris[4 * lt + 3];
+    const int lt = f2i(S.lnodes[node].w);
+    const float4 A = S.ltris[4 * lt], B = S.ltris[4 * lt + 1], C = S.ltris[4 * lt + 2], N = S.ltris[4 * lt + 3];
     const float x = 1.0f - __builtin_sqrtf(g.next());
     const float y = g.next();
     const V3 a{A.x, A.y, A.z}, b{B.x, B.y, B.z}, c{C.x, C.y, C.z};
@@ -149,18 +138,45 @@ __device__ __forceinline__ uint32_t to_u8(float v)
     return ((uint32_t)(int32_t)f) & 0xFFu;
 }
 
-__device__ __forceinline__ uint32_t wave_lane() { return __lane_id(); }
-
 }  // namespace
 
-template <bool EXACT, bool COUNT>
+template <bool EXACT, bool COUNT, bool LDS>
 __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
 {
-    const uint32_t lane = wave_lane();
+    extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
+    SceneView S;
+    S.n_nodes = P.n_nodes;
+    if (LDS) {
+        // stage the whole scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris)
+        const uint32_t nq = 2 * P.n_nodes, tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
+        float4* dn = lds_scene;
+        float4* dt = dn + nq;
+        float4* dm = dt + tq;
+        float4* dl = dm + mq;
+        float4* dlt = dl + lq;
+        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) dn[i] = P.nodes[i];
+        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[i] = P.tris[i];
+        for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
+        for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
+        for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
+        __syncthreads();
+        S.nodes = dn; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt;
+    } else {
+        S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris;
+    }
+
+    const uint32_t lane = __lane_id();
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
+    // EXACT fold stack: levels [0, lds_levels) in LDS ([level][lane] float4 + u8 material), deeper
+    // levels in HBM ([level][thread])
+    float4* lstack = lds_scene + P.lds_scene_quads;
+    uint8_t* lmat = reinterpret_cast<uint8_t*>(lstack + (size_t)P.lds_levels * 256);
+    const uint32_t tib = threadIdx.x;
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
     const float rr = P.rr;
     const V3 cam{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
+    const V3 E{P.light_emission[0], P.light_emission[1], P.light_emission[2]};
+    const float lpdf = 1.0f / P.light_area;   // BVH::Sampling_from_root overwrites PDF (MC/BVH.h:106)
 
     uint32_t node_tests = 0, tri_tests = 0, rays = 0;
     bool alive = true, have_pixel = false, in_path = false;
@@ -169,24 +185,178 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
     Rng g;
     Ray ray;
     uint32_t depth = 0;
-    // pending level (direct radiance of the current bounce, waiting to know whether the indirect ray
-    // continues the path)
+    bool shadow = false;            // the lane's current ray is a shadow ray
+    double slen = 0.0;              // length(q - p) of the shadow ray
+    // shading context carried across the shadow ray: face-forwarded normal, material, and the
+    // occlusion-independent factors of the direct term
+    V3 sn{0, 0, 0}; int smat = 0; float sc1 = 0.0f, sc2 = 0.0f, sd2 = 0.0f;
+    // EXACT: the level waiting to learn whether its indirect ray continues the path
     V3 pend_ld{0, 0, 0}; float pend_cos = 0.0f; int pend_mat = 0;
-    V3 thr{1.0f, 1.0f, 1.0f}, Lsum{0, 0, 0};   // FAST mode
+    // FAST: forward throughput and radiance
+    V3 thr{1.0f, 1.0f, 1.0f}, Lsum{0, 0, 0};
+    // traversal state of the lane's current ray (persists across service rounds)
+    const uint32_t NN = S.n_nodes;
+    uint32_t ti = NN;                        // next node (NN: no ray / finished)
+    double tbest = 1.7976931348623157e308;   // closest t so far (DBL_MAX = IntersectionRecord default)
+    int ttri = -1;                           // closest triangle so far
+    bool toccl = false;                      // shadow ray blocked
+    bool tdone = true;
 
     for (;;) {
-        // ---------------- lane-level work queue (wave-collective)
+        // ======================= service round: lanes whose ray has been traced =======================
+        if (in_path && tdone) {
+            bool finished = false;
+            int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
+            V3 L{0, 0, 0};
+            bool part2 = false;  // run the post-shadow half of shading now
+            bool new_ray = false;
+            V3 ld{0.0f, 0.0f, 0.0f};
+            if (!shadow) {
+                int mat = 0;
+                bool emissive = false;
+                if (ttri >= 0) {
+                    mat = f2i(S.tris[4 * ttri].w);
+                    emissive = S.mats[2 * mat].w != 0.0f;
+                }
+                if (depth == 0) {
+                    if (ttri < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
+                        L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
+                        finished = true;
+                    } else if (emissive) {   // direct emission (MC/Renderer.cpp:151-161)
+                        const float4 em = S.mats[2 * mat + 1];
+                        L = V3{em.x, em.y, em.z};
+                        finished = true;
+                    }
+                } else if (ttri < 0 || emissive) {
+                    // the indirect ray missed or hit the light: radiance_indirect = 0 (MC/Renderer.cpp:202)
+                    L = EXACT ? pend_ld : Lsum;
+                    fold_top = (int)depth - 2;
+                    finished = true;
+                } else if (EXACT) {
+                    // the pending level recurses into this hit: push it as stack level depth-1
+                    const uint32_t lvl = depth - 1;
+                    const float4 e = make_float4(pend_ld.x, pend_ld.y, pend_ld.z, pend_cos);
+                    if (lvl < P.lds_levels) {
+                        lstack[lvl * 256u + tib] = e;
+                        lmat[lvl * 256u + tib] = (uint8_t)pend_mat;
+                    } else if (lvl < P.stack_depth) {
+                        P.stack_ld[(size_t)lvl * P.total_threads + gtid] = e;
+                        P.stack_mat[(size_t)lvl * P.total_threads + gtid] = pend_mat;
+                    } else {
+                        atomicAdd((unsigned long long*)&P.counters[3], 1ull);   // reported as stack overflow
+                    }
+                }
+                if (!finished) {
+                    // ------------ shading, first half (MC/Renderer.cpp:163-186): shading point, light
+                    // sample, shadow ray set-up
+                    const float4 tq3 = S.tris[4 * ttri + 3];
+                    const V3 wo = neg(ray.d);
+                    const V3 loc = add(ray.o, smul((float)tbest, ray.d));   // Ray::operator(), MC/Ray.h:34-37
+                    const V3 N{tq3.x, tq3.y, tq3.z};
+                    const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
+                    const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
+                    sn = n; smat = mat;
+                    if (P.has_light) {
+                        V3 q, nl0;
+                        sample_light(S, P.light_area, g, q, nl0);
+                        const V3 p2q = sub(q, p);
+                        const V3 wl = glm_normalize(p2q);
+                        const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
+                        sc1 = dot(wl, n);
+                        sc2 = dot(neg(wl), nl);
+                        sd2 = dot(p2q, p2q);
+                        slen = (double)glm_length(p2q);
+                        ray = make_ray(p, wl);
+                        shadow = true;
+                        new_ray = true;
+                    } else {
+                        ray.o = p;   // no emitter: direct term 0, continue with roulette
+                        part2 = true;
+                    }
+                }
+            } else {
+                // ------------ the shadow ray came back: direct term (MC/Renderer.cpp:187-189)
+                if (!toccl) {
+                    const float4 mb = S.mats[2 * smat];
+                    const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};   // BRDF, MC/WhittedMaterial.h:58-69
+                    ld = divs(divs(muls(muls(mul(E, f), sc1), sc2), sd2), lpdf);
+                }
+                shadow = false;
+                part2 = true;
+            }
+
+            if (part2) {
+                // ------------ shading, second half: Russian roulette + indirect direction
+                // (MC/Renderer.cpp:193-209; the depth cap only bounds the loop: P(depth > 4096) = rr^4096)
+                if (g.next() < rr && depth < 4096u) {
+                    const V3 wi = glm_normalize(sample_hemisphere(sn, g));
+                    const float c = dot(wi, sn);
+                    if (EXACT) {
+                        pend_ld = ld; pend_cos = c; pend_mat = smat;
+                    } else {
+                        Lsum = add(Lsum, mul(thr, ld));
+                        const float4 mb = S.mats[2 * smat];
+                        const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
+                        thr = muls(mul(thr, f), c / PDF / rr);
+                    }
+                    ray = make_ray(ray.o, wi);
+                    depth = depth + 1;
+                    new_ray = true;
+                } else {
+                    if (EXACT) L = ld;
+                    else { Lsum = add(Lsum, mul(thr, ld)); L = Lsum; }
+                    fold_top = (int)depth - 1;
+                    finished = true;
+                }
+            }
+
+            if (finished) {
+                if (EXACT) {
+                    // fold inner-first: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)   (MC/Renderer.cpp:208,213)
+                    for (int lvl = fold_top; lvl >= 0; --lvl) {
+                        float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+                        int m = 0;
+                        if ((uint32_t)lvl < P.lds_levels) {
+                            e = lstack[(uint32_t)lvl * 256u + tib];
+                            m = lmat[(uint32_t)lvl * 256u + tib];
+                        } else if ((uint32_t)lvl < P.stack_depth) {
+                            e = P.stack_ld[(size_t)lvl * P.total_threads + gtid];
+                            m = P.stack_mat[(size_t)lvl * P.total_threads + gtid];
+                        }
+                        const float4 mb2 = S.mats[2 * m];
+                        const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
+                        L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), rr));
+                    }
+                }
+                // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
+                acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
+                in_path = false;
+                ++k;
+                if (k == P.n_frames) {
+                    const float fr = (float)(P.first_frame + k - 1u);
+                    const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
+                    const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
+                    P.accum[local] = acc;
+                    P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+                    have_pixel = false;
+                }
+            }
+            if (new_ray) {
+                if (COUNT) ++rays;
+                ti = 0; tbest = 1.7976931348623157e308; ttri = -1; toccl = false; tdone = false;
+            }
+        }
+
+        // ======================= lane-level work queue (wave-collective) =======================
         const bool need = alive && !have_pixel;
         const uint64_t mask = __ballot(need);
-        if (mask == 0 && !__any(alive)) break;
         if (mask != 0) {
             uint32_t base = 0;
             const int leader = __ffsll((unsigned long long)mask) - 1;
             if ((int)lane == leader) base = atomicAdd(P.work_counter, (uint32_t)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
-                const uint32_t rank_in = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                const uint32_t w = base + rank_in;
+                const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
                 if (w >= P.n_items) {
                     alive = false;
                 } else {
@@ -208,12 +378,10 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
                 }
             }
         }
-        if (!have_pixel) continue;
 
-        // ---------------- start a new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
-        if (!in_path) {
-            const uint32_t frame = P.first_frame + k;
-            g.start(P.seed, px, frame);
+        // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
+        if (have_pixel && !in_path) {
+            g.start(P.seed, px, P.first_frame + k);
             const float ux = g.next();
             const float uy = g.next();
             float cx = ((float)x + ux) / (float)P.W;
@@ -227,124 +395,63 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             ray = make_ray(cam, w_normalize(V3{wd[0], wd[1], wd[2]}));
             depth = 0;
+            shadow = false;
             in_path = true;
             if (!EXACT) { thr = V3{1.0f, 1.0f, 1.0f}; Lsum = V3{0, 0, 0}; }
+            if (COUNT) ++rays;
+            ti = 0; tbest = 1.7976931348623157e308; ttri = -1; toccl = false; tdone = false;
         }
 
-        // ---------------- one ray segment
-        if (COUNT) ++rays;
-        const Hit h = closest_hit<COUNT>(P, ray, node_tests, tri_tests);
-        bool finished = false;
-        int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
-        V3 L{0, 0, 0};
-        int mat = 0;
-        float4 tq3 = make_float4(0.f, 0.f, 0.f, 0.f);
-        bool emissive = false;
-        if (h.tri >= 0) {
-            mat = f2i(P.tris[4 * h.tri].w);
-            tq3 = P.tris[4 * h.tri + 3];
-            emissive = P.mats[2 * mat].w != 0.0f;
-        }
-        if (depth == 0) {
-            if (h.tri < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
-                L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
-                finished = true;
-            } else if (emissive) {   // shading: direct emission (MC/Renderer.cpp:151-161)
-                const float4 em = P.mats[2 * mat + 1];
-                L = V3{em.x, em.y, em.z};
-                finished = true;
-            }
-        } else if (h.tri < 0 || emissive) {
-            // the indirect ray missed or hit the light: radiance_indirect = 0 (MC/Renderer.cpp:202);
-            // the pending level's radiance is its direct term
-            L = EXACT ? pend_ld : Lsum;
-            fold_top = (int)depth - 2;
-            finished = true;
-        } else if (EXACT) {
-            // the pending level recurses into this hit: push it as stack level depth-1
-            const uint32_t lvl = depth - 1;
-            if (lvl < P.stack_depth) {
-                P.stack_ld[(size_t)lvl * P.total_threads + gtid] = make_float4(pend_ld.x, pend_ld.y, pend_ld.z, pend_cos);
-                P.stack_mat[(size_t)lvl * P.total_threads + gtid] = pend_mat;
-            } else {
-                atomicAdd((unsigned long long*)&P.counters[3], 1ull);   // reported as stack overflow
-            }
-        }
+        if (!__any(have_pixel || alive)) break;
 
-        if (!finished) {
-            // ------------ shading at the hit (MC/Renderer.cpp:163-214)
-            const V3 wo = neg(ray.d);
-            const V3 loc = add(ray.o, smul((float)h.t, ray.d));   // Ray::operator(), MC/Ray.h:34-37
-            const V3 N{tq3.x, tq3.y, tq3.z};
-            const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
-            const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
-            const float4 mb = P.mats[2 * mat];
-            const V3 brdf_m{mb.x, mb.y, mb.z};
-            V3 ld{0.0f, 0.0f, 0.0f};
-            if (P.has_light) {
-                V3 q, nl0;
-                sample_light(P, g, q, nl0);
-                const V3 p2q = sub(q, p);
-                const V3 wl = glm_normalize(p2q);
-                const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
-                if (COUNT) ++rays;
-                const Ray sr = make_ray(p, wl);
-                if (!occluded<COUNT>(P, sr, (double)glm_length(p2q), node_tests, tri_tests)) {
-                    const float c1 = dot(wl, n);
-                    const V3 f = (c1 >= 0.0f) ? brdf_m : V3{0.0f, 0.0f, 0.0f};   // WhittedMaterial::BRDF :58-69
-                    const V3 E{P.light_emission[0], P.light_emission[1], P.light_emission[2]};
-                    const float lpdf = 1.0f / P.light_area;                       // BVH::Sampling_from_root :106
-                    ld = divs(divs(muls(muls(mul(E, f), c1), dot(neg(wl), nl)), dot(p2q, p2q)), lpdf);
-                }
-            }
-            // Russian roulette (MC/Renderer.cpp:193); the depth cap only bounds the loop
-            // (P(depth > 4096) = rr^4096, i.e. 0 for rr <= 0.99)
-            if (g.next() < rr && depth < 4096u) {
-                const V3 wi = glm_normalize(sample_hemisphere(n, g));
-                const float c = dot(wi, n);
-                if (EXACT) {
-                    pend_ld = ld; pend_cos = c; pend_mat = mat;
-                } else {
-                    Lsum = add(Lsum, mul(thr, ld));
-                    const V3 f = (c >= 0.0f) ? brdf_m : V3{0.0f, 0.0f, 0.0f};
-                    thr = muls(mul(thr, f), c / PDF / rr);
-                }
-                ray = make_ray(p, wi);
-                depth = depth + 1;
-            } else {
-                if (EXACT) L = ld;
-                else { Lsum = add(Lsum, mul(thr, ld)); L = Lsum; }
-                fold_top = (int)depth - 1;
-                finished = true;
-            }
-        }
-
-        if (finished) {
-            if (EXACT) {
-                // fold inner-first: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)   (MC/Renderer.cpp:208,213)
-                for (int lvl = fold_top; lvl >= 0; --lvl) {
-                    float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-                    int m = 0;
-                    if ((uint32_t)lvl < P.stack_depth) {
-                        e = P.stack_ld[(size_t)lvl * P.total_threads + gtid];
-                        m = P.stack_mat[(size_t)lvl * P.total_threads + gtid];
+        // ======================= traversal rounds =======================
+        // Rounds continue while more than `thresh` lanes are still tracing, or while nobody waits for
+        // service; then the finished lanes are served while the stragglers keep their traversal state.
+        for (;;) {
+            const bool tracing = in_path && !tdone;
+            const uint64_t act = __ballot(tracing);
+            if (act == 0) break;
+            const uint64_t srv = __ballot((in_path && tdone) || (alive && !have_pixel));
+            if ((uint32_t)__popcll(act) <= P.thresh && srv != 0) break;
+            const bool fin = __all(!tracing || rcp_finite(ray));
+            if (tracing) {
+                int parked = -1;
+                if (fin) {
+                    for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
+                        const float4 q0 = S.nodes[2 * ti];
+                        const float4 q1 = S.nodes[2 * ti + 1];
+                        if (COUNT) ++node_tests;
+                        const bool hit = slab_hit_finite(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                        const int tri = f2i(q1.w);
+                        ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
+                        if (hit && tri >= 0) { parked = tri; break; }
                     }
-                    const float4 mb2 = P.mats[2 * m];
-                    const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                    L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), rr));
+                } else {
+                    for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
+                        const float4 q0 = S.nodes[2 * ti];
+                        const float4 q1 = S.nodes[2 * ti + 1];
+                        if (COUNT) ++node_tests;
+                        const bool hit = slab_hit(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                        const int tri = f2i(q1.w);
+                        ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
+                        if (hit && tri >= 0) { parked = tri; break; }
+                    }
                 }
-            }
-            // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
-            acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
-            in_path = false;
-            ++k;
-            if (k == P.n_frames) {
-                const float fr = (float)(P.first_frame + k - 1u);
-                const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
-                const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
-                P.accum[local] = acc;
-                P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
-                have_pixel = false;
+                if (parked >= 0) {
+                    if (COUNT) ++tri_tests;
+                    const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
+                    double t;
+                    if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, ray, t)) {
+                        if (shadow) {
+                            // not occluded iff length(q-p) < t + 0.01f for every hit (MC/Renderer.cpp:184)
+                            if (!(slen < t + (double)0.01f)) { toccl = true; ti = NN; }
+                        } else if (t <= tbest) {
+                            // (left.t < right.t) ? left : right  ==> the later leaf wins ties
+                            tbest = t; ttri = parked;
+                        }
+                    }
+                }
+                if (ti >= NN) tdone = true;
             }
         }
     }
@@ -363,19 +470,61 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
     }
 }
 
-// explicit instantiations + launchers (C linkage inside rt_capi.cpp)
-template __global__ void pt_megakernel<true, false>(KParams);
-template __global__ void pt_megakernel<true, true>(KParams);
-template __global__ void pt_megakernel<false, false>(KParams);
-template __global__ void pt_megakernel<false, true>(KParams);
+#define RT_INST(E, C, L) template __global__ void pt_megakernel<E, C, L>(KParams);
+RT_INST(true, false, true) RT_INST(true, true, true) RT_INST(false, false, true) RT_INST(false, true, true)
+RT_INST(true, false, false) RT_INST(true, true, false) RT_INST(false, false, false) RT_INST(false, true, false)
 
-hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, uint32_t grid, uint32_t block, hipStream_t stream)
+namespace {
+template <bool E, bool C, bool L>
+hipError_t launch_one(const KParams& P, uint32_t grid, uint32_t block, size_t lds, hipStream_t s)
 {
-    if (exact && count) hipLaunchKernelGGL((pt_megakernel<true, true>), dim3(grid), dim3(block), 0, stream, P);
-    else if (exact) hipLaunchKernelGGL((pt_megakernel<true, false>), dim3(grid), dim3(block), 0, stream, P);
-    else if (count) hipLaunchKernelGGL((pt_megakernel<false, true>), dim3(grid), dim3(block), 0, stream, P);
-    else hipLaunchKernelGGL((pt_megakernel<false, false>), dim3(grid), dim3(block), 0, stream, P);
+    hipLaunchKernelGGL((pt_megakernel<E, C, L>), dim3(grid), dim3(block), lds, s, P);
     return hipGetLastError();
+}
+template <bool E, bool C, bool L>
+int occ_one(int block, size_t lds)
+{
+    int n = 0;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_megakernel<E, C, L>, block, lds) == hipSuccess ? n : 0;
+}
+}  // namespace
+
+size_t rt_stack_lds_bytes(uint32_t levels) { return (size_t)levels * 256 * (sizeof(float4) + 1); }
+
+size_t rt_scene_lds_bytes(const KParams& P)
+{
+    return (size_t)(2 * P.n_nodes + 4 * P.n_tris + 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris) * sizeof(float4);
+}
+
+hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream)
+{
+    const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
+    const int sel = (exact ? 4 : 0) | (count ? 2 : 0) | (lds ? 1 : 0);
+    switch (sel) {
+        case 7: return launch_one<true, true, true>(P, grid, block, sh, stream);
+        case 6: return launch_one<true, true, false>(P, grid, block, sh, stream);
+        case 5: return launch_one<true, false, true>(P, grid, block, sh, stream);
+        case 4: return launch_one<true, false, false>(P, grid, block, sh, stream);
+        case 3: return launch_one<false, true, true>(P, grid, block, sh, stream);
+        case 2: return launch_one<false, true, false>(P, grid, block, sh, stream);
+        case 1: return launch_one<false, false, true>(P, grid, block, sh, stream);
+        default: return launch_one<false, false, false>(P, grid, block, sh, stream);
+    }
+}
+
+int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes)
+{
+    const int sel = (exact ? 4 : 0) | (count ? 2 : 0) | (lds ? 1 : 0);
+    switch (sel) {
+        case 7: return occ_one<true, true, true>(block, lds_bytes);
+        case 6: return occ_one<true, true, false>(block, 0);
+        case 5: return occ_one<true, false, true>(block, lds_bytes);
+        case 4: return occ_one<true, false, false>(block, 0);
+        case 3: return occ_one<false, true, true>(block, lds_bytes);
+        case 2: return occ_one<false, true, false>(block, 0);
+        case 1: return occ_one<false, false, true>(block, lds_bytes);
+        default: return occ_one<false, false, false>(block, 0);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -385,11 +534,15 @@ __global__ void __launch_bounds__(256) trace_kernel(KParams P, uint32_t n, const
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    SceneView S{P.nodes, P.tris, P.mats, P.lnodes, P.ltris, P.n_nodes};
     const Ray r = make_ray(V3{org[3 * i], org[3 * i + 1], org[3 * i + 2]}, V3{dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]});
     uint32_t a = 0, b = 0;
-    const Hit h = closest_hit<false>(P, r, a, b);
-    tri_out[i] = h.tri;
-    t_out[i] = h.tri >= 0 ? h.t : 1.7976931348623157e308;
+    double best = 1.7976931348623157e308;
+    int best_tri = -1;
+    bool occl = false;
+    traverse_impl<false, false>(S, r, false, 0.0, best, best_tri, occl, a, b);
+    tri_out[i] = best_tri;
+    t_out[i] = best_tri >= 0 ? best : 1.7976931348623157e308;
 }
 
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream)
@@ -420,15 +573,4 @@ hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t st
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(math_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, x, out);
     return hipGetLastError();
-}
-
-int rt_megakernel_occupancy(bool exact, bool count, int block)
-{
-    int n = 0;
-    hipError_t e;
-    if (exact && count) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_megakernel<true, true>, block, 0);
-    else if (exact) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_megakernel<true, false>, block, 0);
-    else if (count) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_megakernel<false, true>, block, 0);
-    else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_megakernel<false, false>, block, 0);
-    return e == hipSuccess ? n : 0;
 }

@@ -92,6 +92,8 @@ uint32_t rt_local_rows(const rt_ctx* ctx);
 
 #define RT_RENDER_EXACT 1u /* fold the recursion inner-first (bit-faithful accumulation); else forward */
 #define RT_RENDER_COUNT 2u /* collect node/triangle/ray counters (rt_get_stats) */
+#define RT_RENDER_GLOBAL_SCENE 4u /* read the scene from HBM even when it fits in LDS (A/B) */
+#define RT_RENDER_GLOBAL_STACK 8u /* keep the whole EXACT fold stack in HBM (A/B) */
 typedef struct {
     uint32_t first_frame; /* 1-based frame index of the first sample (== reference frame_accumulating) */
     uint32_t n_frames;    /* samples per pixel rendered by this call */

@@ -137,3 +137,16 @@ def test_counters_and_no_stack_overflow(ctx):
     assert st.samples == 64 * 64 * 16 and st.stack_overflows == 0
     assert 4.0 < st.rays / st.samples < 7.5
     assert st.node_tests > st.rays and st.tri_tests > 0 and st.last_kernel_ms > 0
+
+
+def test_exact_modes_agree_bitwise(ctx):
+    # scene in LDS or HBM, fold stack in LDS or HBM: the same IEEE operations, the same bits
+    W, H, spp = 96, 80, 24
+    ctx.resize(W, H)
+    cam, _, _ = rt.camera_default(W, H)
+    ref = None
+    for kw in (dict(), dict(global_scene=True), dict(global_stack=True), dict(global_scene=True, global_stack=True)):
+        rgba, acc = ctx.render(cam, spp, seed=9, **kw)
+        if ref is None:
+            ref = acc
+        assert np.array_equal(bits(acc), bits(ref)), kw
