@@ -44,7 +44,8 @@ class RenderParams(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("last_kernel_ms", C.c_float), ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("rays", C.c_uint64),
                 ("stack_overflows", C.c_uint64), ("samples", C.c_uint64), ("grid", C.c_uint32), ("block", C.c_uint32),
-                ("stack_depth", C.c_uint32)]
+                ("stack_depth", C.c_uint32), ("wave_rounds", C.c_uint64), ("wave_steps", C.c_uint64),
+                ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64)]
 
 
 class SceneInfo(C.Structure):

@@ -46,7 +46,7 @@ struct rt_ctx {
     rt_stats stats{};
     bool pending_stats = false;
     uint32_t last_flags = 0;
-    uint32_t thresh = 8, steps = 8;    // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
+    uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
 
 namespace {
@@ -188,7 +188,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
         c->own_stream = true;
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 64) != hipSuccess) {
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 128) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
         return RT_ERR_HIP;
@@ -318,9 +318,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
     if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
-        const size_t budget = 40 * 1024, used = lds ? lds_bytes : 0;
+        const size_t used = lds ? lds_bytes : 0;
+        const int occ0 = rt_megakernel_occupancy(exact, count, lds, (int)c->block, used);
         for (uint32_t lv = 8; lv > 0; --lv)
-            if (used + rt_stack_lds_bytes(lv) <= budget) { P.lds_levels = lv; break; }
+            if (rt_megakernel_occupancy(exact, count, lds, (int)c->block, used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
     int bpc = rt_megakernel_occupancy(exact, count, lds, (int)c->block, shmem);
@@ -328,7 +329,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
     HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 64, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 128, c->stream));
     c->last_flags = p->flags;
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
@@ -384,9 +385,10 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_kernel_ms = ms;
-        unsigned long long h[4] = {0, 0, 0, 0};
+        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         HIPC(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
         c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[3];
+        c->stats.wave_rounds = h[4]; c->stats.wave_steps = h[5]; c->stats.wave_tri_tests = h[6]; c->stats.wave_service = h[7];
         c->pending_stats = false;
     }
     c->stats.block = c->block; c->stats.stack_depth = c->stack_depth;

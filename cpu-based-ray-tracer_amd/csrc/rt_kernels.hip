@@ -179,6 +179,8 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
     const float lpdf = 1.0f / P.light_area;   // BVH::Sampling_from_root overwrites PDF (MC/BVH.h:106)
 
     uint32_t node_tests = 0, tri_tests = 0, rays = 0;
+    // COUNT diagnostics: wave-level executions (counted by the first active lane)
+    uint32_t w_rounds = 0, w_steps = 0, w_mt = 0, w_service = 0, w_fold = 0;
     bool alive = true, have_pixel = false, in_path = false;
     uint32_t local = 0, px = 0, x = 0, y = 0, k = 0;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -204,6 +206,7 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
 
     for (;;) {
         // ======================= service round: lanes whose ray has been traced =======================
+        if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_service;
         if (in_path && tdone) {
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
@@ -314,6 +317,7 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
                 if (EXACT) {
                     // fold inner-first: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)   (MC/Renderer.cpp:208,213)
                     for (int lvl = fold_top; lvl >= 0; --lvl) {
+                        if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_fold;
                         float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
                         int m = 0;
                         if ((uint32_t)lvl < P.lds_levels) {
@@ -414,31 +418,42 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             const uint64_t srv = __ballot((in_path && tdone) || (alive && !have_pixel));
             if ((uint32_t)__popcll(act) <= P.thresh && srv != 0) break;
             const bool fin = __all(!tracing || rcp_finite(ray));
+            if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_rounds;
             if (tracing) {
-                int parked = -1;
+                // box steps; up to two leaves are parked (in DFS order) before the lane stops
+                int parked0 = -1, parked1 = -1;
                 if (fin) {
                     for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
                         const float4 q0 = S.nodes[2 * ti];
                         const float4 q1 = S.nodes[2 * ti + 1];
-                        if (COUNT) ++node_tests;
+                        if (COUNT) { ++node_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_steps; }
                         const bool hit = slab_hit_finite(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                         const int tri = f2i(q1.w);
                         ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
-                        if (hit && tri >= 0) { parked = tri; break; }
+                        if (hit && tri >= 0) {
+                            if (parked0 < 0) parked0 = tri;
+                            else { parked1 = tri; break; }
+                        }
                     }
                 } else {
                     for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
                         const float4 q0 = S.nodes[2 * ti];
                         const float4 q1 = S.nodes[2 * ti + 1];
-                        if (COUNT) ++node_tests;
+                        if (COUNT) { ++node_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_steps; }
                         const bool hit = slab_hit(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                         const int tri = f2i(q1.w);
                         ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
-                        if (hit && tri >= 0) { parked = tri; break; }
+                        if (hit && tri >= 0) {
+                            if (parked0 < 0) parked0 = tri;
+                            else { parked1 = tri; break; }
+                        }
                     }
                 }
-                if (parked >= 0) {
-                    if (COUNT) ++tri_tests;
+                // intersect the parked triangles in order
+                for (int slot = 0; slot < 2; ++slot) {
+                    const int parked = slot == 0 ? parked0 : parked1;
+                    if (parked < 0 || toccl) continue;
+                    if (COUNT) { ++tri_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_mt; }
                     const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
                     double t;
                     if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, ray, t)) {
@@ -462,10 +477,21 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
         for (int off = 32; off > 0; off >>= 1) {
             a += __shfl_down(a, off); b += __shfl_down(b, off); c += __shfl_down(c, off);
         }
+        // wave-level counts live in exactly one lane: the sum is the wave's count
+        uint64_t wr = w_rounds, ws = w_steps, wm = w_mt, wv = w_service, wf = w_fold;
+        for (int off = 32; off > 0; off >>= 1) {
+            wr += __shfl_down(wr, off); ws += __shfl_down(ws, off); wm += __shfl_down(wm, off);
+            wv += __shfl_down(wv, off); wf += __shfl_down(wf, off);
+        }
         if (lane == 0) {
             atomicAdd((unsigned long long*)&P.counters[0], (unsigned long long)a);
             atomicAdd((unsigned long long*)&P.counters[1], (unsigned long long)b);
             atomicAdd((unsigned long long*)&P.counters[2], (unsigned long long)c);
+            atomicAdd((unsigned long long*)&P.counters[4], (unsigned long long)wr);
+            atomicAdd((unsigned long long*)&P.counters[5], (unsigned long long)ws);
+            atomicAdd((unsigned long long*)&P.counters[6], (unsigned long long)wm);
+            atomicAdd((unsigned long long*)&P.counters[7], (unsigned long long)wv);
+            atomicAdd((unsigned long long*)&P.counters[8], (unsigned long long)wf);
         }
     }
 }

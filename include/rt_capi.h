@@ -122,6 +122,8 @@ typedef struct {
     uint64_t stack_overflows; /* paths deeper than the EXACT fold stack (expected 0) */
     uint64_t samples;
     uint32_t grid, block, stack_depth;
+    /* RT_RENDER_COUNT scheduling diagnostics: wave-level executions */
+    uint64_t wave_rounds, wave_steps, wave_tri_tests, wave_service;
 } rt_stats;
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 

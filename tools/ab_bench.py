@@ -56,7 +56,10 @@ def main():
             ctx.render(cam, spp, fetch=False, count=True, **VARIANTS[n])
             st = ctx.stats()
             out[n].update(rays_per_sample=st.rays / st.samples, nodes_per_ray=st.node_tests / st.rays, tris_per_ray=st.tri_tests / st.rays,
-                          grid=st.grid)
+                          grid=st.grid, step_lane_eff=st.node_tests / max(1, 64 * st.wave_steps),
+                          mt_lane_eff=st.tri_tests / max(1, 64 * st.wave_tri_tests),
+                          wave_steps_per_sample=st.wave_steps / st.samples, wave_mt_per_sample=st.wave_tri_tests / st.samples,
+                          wave_rounds_per_sample=st.wave_rounds / st.samples, wave_service_per_sample=st.wave_service / st.samples)
     base = images[names[0]].view(np.uint32)
     for n in names[1:]:
         out[n]["bitwise_equal_to_" + names[0]] = bool(np.array_equal(images[n].view(np.uint32), base))
