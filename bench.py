@@ -42,13 +42,12 @@ def load_pkg():
     return m
 
 
-def local_rows_of(H, band, rank, nranks):
-    rows = []
-    b = rank
-    while b * band < H:
-        rows.extend(range(b * band, min((b + 1) * band, H)))
-        b += nranks
-    return rows
+def load_dist():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rt_dist", os.path.join(REPO, "cpu-based-ray-tracer_amd", "dist.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
 
 
 def cpu_baseline(W, H, seconds, threads):
@@ -136,29 +135,15 @@ def main():
     ctx.resize(W, H, args.band, rank, world)
     cam, _, _ = rt.camera_default(W, H)
 
-    rows_all = [local_rows_of(H, args.band, r, world) for r in range(world)]
-    max_rows = max(len(r) for r in rows_all)
-    send = torch.zeros(max_rows * W, dtype=torch.int32, device=dev)
-    recv = torch.zeros(world * max_rows * W, dtype=torch.int32, device=dev) if world > 1 else send
-    image = torch.zeros(H * W, dtype=torch.int32, device=dev)
-    # gathered slot (rank r, local row i) -> global row
-    src_idx, dst_idx = [], []
-    for r in range(world):
-        for i, y in enumerate(rows_all[r]):
-            src_idx.append(r * max_rows + i)
-            dst_idx.append(y)
-    src_rows = torch.tensor(src_idx, dtype=torch.int64, device=dev)
-    dst_rows = torch.tensor(dst_idx, dtype=torch.int64, device=dev)
-
+    rtdist = load_dist()
+    gat = rtdist.ImageGather(W, H, args.band, rank, world, dev)
+    assert gat.n_local == ctx.local_rows
     kernel_ms = []
 
     def step():
         ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not args.fast, fetch=False)
-        ctx.copy_rgba_to_device(send.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(recv, send)
-        if rank == 0:
-            image.view(H, W).index_copy_(0, dst_rows, recv.view(-1, W).index_select(0, src_rows))
+        ctx.copy_rgba_to_device(gat.send.data_ptr())   # this rank's rows, on the shared stream
+        gat.gather()                                    # RCCL all-gather + reassembly on rank 0
         kernel_ms.append(ctx.stats().last_kernel_ms)
 
     for _ in range(args.warmup):
@@ -185,7 +170,7 @@ def main():
     value = total_samples / elapsed / 1e6
 
     # roofline of the megakernel on this rank: algorithmic bytes per launch / mean launch time
-    local_samples = len(rows_all[rank]) * W * spp
+    local_samples = gat.n_local * W * spp
     k_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
     achieved = BYTES_PER_SAMPLE * local_samples / k_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
