@@ -207,6 +207,14 @@ void Renderer::RenderFrames(const Camera& camera, uint32_t n)
     if (!frame_image_final) throw rt::Error("Render before ResizeViewport");
     if (bvh_dirty) GenerateBVH();
     const rt_camera cam = camera.Native();
+    if (!settings.accumulating) {
+        // every frame restarts the average (frame_accumulating stays 1, MC/Renderer.cpp:95-98,114-121),
+        // so only the last of n frames is visible: render that one, on a fresh RNG epoch so
+        // successive frames carry fresh noise like the reference's free-running mt19937
+        if (n == 0) return;
+        ++epoch;
+        n = 1;
+    }
     rt_render_params p{frame_accumulating, n, settings.seed + epoch, RR_survival_probability, settings.exact ? RT_RENDER_EXACT : 0u};
     check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
     if (settings.accumulating) frame_accumulating += n;
