@@ -21,6 +21,7 @@ RENDER_EXACT = 1
 RENDER_COUNT = 2
 RENDER_GLOBAL_SCENE = 4
 RENDER_GLOBAL_STACK = 8
+RENDER_WHITTED = 16
 
 _lib = None
 
@@ -45,7 +46,9 @@ class Stats(C.Structure):
     _fields_ = [("last_kernel_ms", C.c_float), ("node_tests", C.c_uint64), ("tri_tests", C.c_uint64), ("rays", C.c_uint64),
                 ("stack_overflows", C.c_uint64), ("samples", C.c_uint64), ("grid", C.c_uint32), ("block", C.c_uint32),
                 ("stack_depth", C.c_uint32), ("wave_rounds", C.c_uint64), ("wave_steps", C.c_uint64),
-                ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64)]
+                ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64), ("wave_fold", C.c_uint64),
+                ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
+                ("service_lanes", C.c_uint64)]
 
 
 class SceneInfo(C.Structure):
@@ -73,6 +76,11 @@ def lib():
         "rt_scene_add_cornell_box": (i32, [vp]),
         "rt_scene_add_obj": (i32, [vp, C.c_char_p, fp, fp, C.POINTER(i32)]),
         "rt_scene_add_mesh": (i32, [vp, fp, u64, fp, fp, C.POINTER(i32)]),
+        "rt_scene_add_whitted_mesh": (i32, [vp, fp, u64, C.c_float, fp, fp, C.c_float, C.POINTER(i32)]),
+        "rt_scene_add_whitted_obj": (i32, [vp, C.c_char_p, C.c_float, fp, fp, C.c_float, C.POINTER(i32)]),
+        "rt_scene_add_point_light": (i32, [vp, fp, fp]),
+        "rt_scene_set_sky": (i32, [vp, fp]),
+        "rt_scene_add_bvh_tracer_scene": (i32, [vp, C.c_char_p, C.c_char_p]),
         "rt_scene_build": (i32, [vp]),
         "rt_scene_get_info": (i32, [vp, C.POINTER(SceneInfo)]),
         "rt_scene_export": (i32, [vp, fp, C.POINTER(i32), fp, C.POINTER(i32)]),
@@ -136,6 +144,32 @@ class Scene:
                                            _fp(np.asarray(emission, np.float32)), C.byref(mid)), "rt_scene_add_obj")
         return mid.value
 
+    # ---- Whitted-style scenes (the reference's BVH Ray Tracer, BV/Renderer.cpp:26-43)
+    def add_whitted_mesh(self, raw, scale, offset, diffuse=(0.5, 0.5, 0.5), phong_diffuse=0.6):
+        raw = np.ascontiguousarray(raw, np.float32).reshape(-1, 9)
+        off = None if offset is None else _fp(np.asarray(offset, np.float32))
+        mid = C.c_int32()
+        self._check(lib().rt_scene_add_whitted_mesh(self.h, _fp(raw), raw.shape[0], float(scale), off, _fp(np.asarray(diffuse, np.float32)),
+                                                    float(phong_diffuse), C.byref(mid)), "rt_scene_add_whitted_mesh")
+        return mid.value
+
+    def add_point_light(self, position, radiance=(1.0, 1.0, 1.0)):
+        self._check(lib().rt_scene_add_point_light(self.h, _fp(np.asarray(position, np.float32)), _fp(np.asarray(radiance, np.float32))),
+                    "rt_scene_add_point_light")
+
+    def set_sky(self, rgb):
+        self._check(lib().rt_scene_set_sky(self.h, _fp(np.asarray(rgb, np.float32))), "rt_scene_set_sky")
+
+    @classmethod
+    def bvh_tracer(cls, bunny_raw, teapot_raw):
+        """The BVH Ray Tracer's Renderer::Renderer() scene from raw objl positions (BV/Renderer.cpp:26-43)."""
+        s = cls()
+        s.add_whitted_mesh(bunny_raw, 2.0, (-1.0, 6.1, 0.0))
+        s.add_whitted_mesh(teapot_raw, 1.0, (-1.0, 3.0, 0.0))
+        s.add_point_light((-20.0, 70.0, 20.0))
+        s.add_point_light((20.0, 70.0, 20.0))
+        return s.build()
+
     def build(self):
         self._check(lib().rt_scene_build(self.h), "rt_scene_build")
         return self
@@ -160,6 +194,20 @@ class Scene:
                 self.h = C.c_void_p()
         except Exception:
             pass
+
+
+def camera_look(W, H, position, forward, vfov=35.0, near=0.1, far=100.0):
+    cam = Camera()
+    st = lib().rt_camera_look(W, H, _fp(np.asarray(position, np.float32)), _fp(np.asarray(forward, np.float32)), vfov, near, far,
+                              C.byref(cam))
+    if st != RT_OK:
+        raise RtError(f"rt_camera_look failed {st}")
+    return cam
+
+
+def camera_bvh_tracer(W, H):
+    """The BVH Ray Tracer's Camera{35, 0.1, 100} at (-1, 5, 10) looking down -z (BV/Camera.h:19-20, BV/mainloop.cpp:22)."""
+    return camera_look(W, H, (-1.0, 5.0, 10.0), (0.0, 0.0, -1.0))
 
 
 def camera_default(W, H):
@@ -198,9 +246,9 @@ class Context:
         self.local_rows = lib().rt_local_rows(self.h)
 
     def render(self, cam, n_frames, first_frame=1, seed=0, rr=0.8, exact=True, count=False, fetch=True, global_scene=False,
-               global_stack=False):
+               global_stack=False, whitted=False):
         flags = (RENDER_EXACT if exact else 0) | (RENDER_COUNT if count else 0) | (RENDER_GLOBAL_SCENE if global_scene else 0)
-        flags |= RENDER_GLOBAL_STACK if global_stack else 0
+        flags |= (RENDER_GLOBAL_STACK if global_stack else 0) | (RENDER_WHITTED if whitted else 0)
         p = RenderParams(first_frame, n_frames, seed, rr, flags)
         if fetch:
             rgba = np.zeros((self.local_rows, self.W), np.uint32)

@@ -27,6 +27,7 @@ struct rt_ctx {
     std::string err;
     // scene
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr;
+    float4 *d_wmats = nullptr, *d_plights = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
     // image
@@ -133,6 +134,65 @@ rt_status rt_scene_add_obj(rt_scene* s, const char* path, const float albedo[3],
     return RT_OK;
 }
 
+rt_status rt_scene_add_whitted_mesh(rt_scene* s, const float* raw, uint64_t n_tris, float scale, const float offset[3], const float diffuse[3],
+                                    float phong_diffuse, int32_t* mesh_id)
+{
+    if (!s || !raw || n_tris == 0 || !diffuse) return RT_ERR_INVALID;
+    rt::MeshDesc m;
+    m.raw.assign(raw, raw + 9 * n_tris);
+    m.material = rt::MaterialDesc{{diffuse[0], diffuse[1], diffuse[2]}, {0, 0, 0}, phong_diffuse};
+    m.scale = scale;
+    if (offset) { m.has_offset = true; m.offset = rt::F3{offset[0], offset[1], offset[2]}; }
+    m.name = "whitted" + std::to_string(s->builder.num_meshes());
+    const int id = s->builder.add_mesh(std::move(m));
+    if (mesh_id) *mesh_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_whitted_obj(rt_scene* s, const char* path, float scale, const float offset[3], const float diffuse[3], float phong_diffuse,
+                                   int32_t* mesh_id)
+{
+    if (!s || !path || !diffuse) return RT_ERR_INVALID;
+    std::vector<float> raw;
+    std::string err;
+    if (!rt::SceneBuilder::load_obj_positions(path, raw, err) || raw.empty()) return RT_ERR_IO;
+    return rt_scene_add_whitted_mesh(s, raw.data(), raw.size() / 9, scale, offset, diffuse, phong_diffuse, mesh_id);
+}
+
+rt_status rt_scene_add_point_light(rt_scene* s, const float position[3], const float radiance[3])
+{
+    if (!s || !position || !radiance) return RT_ERR_INVALID;
+    s->builder.add_point_light(rt::PointLight{{position[0], position[1], position[2]}, {radiance[0], radiance[1], radiance[2]}});
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_set_sky(rt_scene* s, const float rgb[3])
+{
+    if (!s || !rgb) return RT_ERR_INVALID;
+    s->builder.set_sky(rt::F3{rgb[0], rgb[1], rgb[2]});
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_bvh_tracer_scene(rt_scene* s, const char* bunny_obj, const char* teapot_obj)
+{
+    // Renderer::Renderer(), BV/Renderer.cpp:26-43: bunny x2 at (-1, 6.1, 0), teapot x1 at (-1, 3, 0),
+    // Diffuse_Glossy triangles with diffuse color 0.5 and phong_diffuse 0.6 (BV/TriangleMesh.h:64-67,138-141),
+    // point lights (-20, 70, 20) and (20, 70, 20) of radiance 1
+    if (!s || !bunny_obj || !teapot_obj) return RT_ERR_INVALID;
+    const float grey[3] = {0.5f, 0.5f, 0.5f};
+    const float ob[3] = {-1.0f, 6.1f, 0.0f}, ot[3] = {-1.0f, 3.0f, 0.0f};
+    rt_status r;
+    if ((r = rt_scene_add_whitted_obj(s, bunny_obj, 2.0f, ob, grey, 0.6f, nullptr)) != RT_OK) return r;
+    if ((r = rt_scene_add_whitted_obj(s, teapot_obj, 1.0f, ot, grey, 0.6f, nullptr)) != RT_OK) return r;
+    const float l0[3] = {-20.0f, 70.0f, 20.0f}, l1[3] = {20.0f, 70.0f, 20.0f}, one[3] = {1.0f, 1.0f, 1.0f};
+    rt_scene_add_point_light(s, l0, one);
+    rt_scene_add_point_light(s, l1, one);
+    return RT_OK;
+}
+
 rt_status rt_scene_build(rt_scene* s)
 {
     if (!s) return RT_ERR_INVALID;
@@ -188,7 +248,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
         c->own_stream = true;
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 128) != hipSuccess) {
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 256) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
         return RT_ERR_HIP;
@@ -221,7 +281,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris);
+    dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -243,6 +303,8 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_mats, s->flat.mats)) != RT_OK) return r;
     if ((r = upload(c, c->d_lnodes, s->flat.lnodes)) != RT_OK) return r;
     if ((r = upload(c, c->d_ltris, s->flat.ltris)) != RT_OK) return r;
+    if ((r = upload(c, c->d_wmats, s->flat.wmats)) != RT_OK) return r;
+    if ((r = upload(c, c->d_plights, s->flat.plights)) != RT_OK) return r;
     c->hdr = s->flat.hdr;
     c->has_scene = true;
     return RT_OK;
@@ -276,9 +338,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (p->first_frame == 0) { c->err = "first_frame is 1-based"; return RT_ERR_INVALID; }
     // a survival probability >= 1 never terminates a path in a closed scene (the reference recurses
     // until its stack overflows); reject it, and NaN
-    if (!(p->rr >= 0.0f && p->rr < 1.0f)) { c->err = "rr must be in [0, 1)"; return RT_ERR_INVALID; }
+    if (!(p->flags & RT_RENDER_WHITTED) && !(p->rr >= 0.0f && p->rr < 1.0f)) { c->err = "rr must be in [0, 1)"; return RT_ERR_INVALID; }
     HIPC(c, hipSetDevice(c->device));
-    const bool exact = (p->flags & RT_RENDER_EXACT) != 0, count = (p->flags & RT_RENDER_COUNT) != 0;
+    const bool whitted = (p->flags & RT_RENDER_WHITTED) != 0;
+    const bool exact = !whitted && (p->flags & RT_RENDER_EXACT) != 0, count = (p->flags & RT_RENDER_COUNT) != 0;
     if (exact && !c->d_stack_ld) {
         c->stack_depth = kStackDepth;
         HIPC(c, hipMalloc((void**)&c->d_stack_ld, (size_t)c->stack_depth * c->total_threads * sizeof(float4)));
@@ -293,6 +356,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.light_area = c->hdr.light_area;
     std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
     P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;
+    P.wmats = c->d_wmats; P.plights = c->d_plights; P.n_plights = c->hdr.n_plights;
+    std::memcpy(P.sky, c->hdr.sky, sizeof P.sky);
     std::memcpy(P.cam_pos, cam->position, sizeof P.cam_pos);
     std::memcpy(P.iproj, cam->inv_projection, sizeof P.iproj);
     std::memcpy(P.iview, cam->inv_view, sizeof P.iview);
@@ -329,11 +394,15 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
     HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 128, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 256, c->stream));
     c->last_flags = p->flags;
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
-        HIPC(c, rt_launch_megakernel(P, exact, count, lds, grid, c->block, c->stream));
+        if (whitted) {
+            HIPC(c, rt_launch_whitted(P, count, c->stream, &grid));
+        } else {
+            HIPC(c, rt_launch_megakernel(P, exact, count, lds, grid, c->block, c->stream));
+        }
         c->stats.grid = grid;
         HIPC(c, hipEventRecord(c->ev1, c->stream));
         c->pending_stats = true;
@@ -385,10 +454,12 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_kernel_ms = ms;
-        unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long h[16] = {};
         HIPC(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
         c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[3];
         c->stats.wave_rounds = h[4]; c->stats.wave_steps = h[5]; c->stats.wave_tri_tests = h[6]; c->stats.wave_service = h[7];
+        c->stats.wave_fold = h[8]; c->stats.cycles_service = h[9]; c->stats.cycles_queue = h[10]; c->stats.cycles_trace = h[11];
+        c->stats.service_lanes = h[12];
         c->pending_stats = false;
     }
     c->stats.block = c->block; c->stats.stack_depth = c->stack_depth;

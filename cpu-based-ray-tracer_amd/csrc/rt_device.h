@@ -227,6 +227,13 @@ __device__ __forceinline__ float sin_f(float y)
     return (float)r;
 }
 
+__device__ __forceinline__ uint32_t to_u8(float v)
+{   // (uint8_t)(c * 255.0f), MC/Renderer.cpp:17-20 (v in [0,1] after clamp; NaN -> 0 like x86 cvttss2si)
+    const float f = v * 255.0f;
+    if (!(f == f)) return 0u;
+    return ((uint32_t)(int32_t)f) & 0xFFu;
+}
+
 // glm mat4 * vec4, GLM/detail/type_mat4x4.inl:561-572: (m0*v0 + m1*v1) + (m2*v2 + m3*v3); m column-major
 __device__ __forceinline__ void mat4_mul(const float* m, float v0, float v1, float v2, float v3, float out[4])
 {

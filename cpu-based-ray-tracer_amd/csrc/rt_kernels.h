@@ -12,6 +12,8 @@ struct KParams {
     const float4* lnodes; uint32_t n_lnodes;
     const float4* ltris; uint32_t n_ltris;
     float light_area; float light_emission[3]; int has_light;
+    // Whitted shading (rt_whitted.hip): per-material (diffuse color, phong_diffuse), point lights, sky
+    const float4* wmats; const float4* plights; uint32_t n_plights; float sky[3];
     // camera: position, inverse projection, inverse view (column-major glm mat4)
     float cam_pos[3]; float iproj[16]; float iview[16];
     // image and sampling
@@ -39,6 +41,8 @@ size_t rt_scene_lds_bytes(const KParams& P);
 size_t rt_stack_lds_bytes(uint32_t levels);
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
+// Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
+hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);
 

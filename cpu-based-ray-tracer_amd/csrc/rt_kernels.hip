@@ -131,13 +131,6 @@ __device__ __forceinline__ V3 sample_hemisphere(V3 n, Rng& g)
     return add(add(smul(x, X), smul(y, Y)), smul(z, n));
 }
 
-__device__ __forceinline__ uint32_t to_u8(float v)
-{   // (uint8_t)(c * 255.0f), MC/Renderer.cpp:17-20 (v in [0,1] after clamp; NaN -> 0 like x86 cvttss2si)
-    const float f = v * 255.0f;
-    if (!(f == f)) return 0u;
-    return ((uint32_t)(int32_t)f) & 0xFFu;
-}
-
 }  // namespace
 
 template <bool EXACT, bool COUNT, bool LDS>
@@ -204,9 +197,15 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
     bool toccl = false;                      // shadow ray blocked
     bool tdone = true;
 
+    uint64_t c_service = 0, c_queue = 0, c_trace = 0, s_lanes = 0;   // COUNT: wave-uniform cycle sums
     for (;;) {
         // ======================= service round: lanes whose ray has been traced =======================
-        if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_service;
+        uint64_t tc0 = 0;
+        if (COUNT) {
+            tc0 = clock64();
+            if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_service;
+            s_lanes += (uint64_t)__popcll(__ballot(in_path && tdone));
+        }
         if (in_path && tdone) {
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
@@ -351,6 +350,8 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             }
         }
 
+        uint64_t tc1 = 0;
+        if (COUNT) { tc1 = clock64(); c_service += tc1 - tc0; }
         // ======================= lane-level work queue (wave-collective) =======================
         const bool need = alive && !have_pixel;
         const uint64_t mask = __ballot(need);
@@ -406,6 +407,8 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             ti = 0; tbest = 1.7976931348623157e308; ttri = -1; toccl = false; tdone = false;
         }
 
+        uint64_t tc2 = 0;
+        if (COUNT) { tc2 = clock64(); c_queue += tc2 - tc1; }
         if (!__any(have_pixel || alive)) break;
 
         // ======================= traversal rounds =======================
@@ -469,6 +472,7 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
                 if (ti >= NN) tdone = true;
             }
         }
+        if (COUNT) c_trace += clock64() - tc2;
     }
 
     if (COUNT) {
@@ -484,6 +488,10 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             wv += __shfl_down(wv, off); wf += __shfl_down(wf, off);
         }
         if (lane == 0) {
+            atomicAdd((unsigned long long*)&P.counters[9], (unsigned long long)c_service);
+            atomicAdd((unsigned long long*)&P.counters[10], (unsigned long long)c_queue);
+            atomicAdd((unsigned long long*)&P.counters[11], (unsigned long long)c_trace);
+            atomicAdd((unsigned long long*)&P.counters[12], (unsigned long long)s_lanes);
             atomicAdd((unsigned long long*)&P.counters[0], (unsigned long long)a);
             atomicAdd((unsigned long long*)&P.counters[1], (unsigned long long)b);
             atomicAdd((unsigned long long*)&P.counters[2], (unsigned long long)c);

@@ -21,6 +21,10 @@
 //  lnodes  : light-mesh BVH for area sampling (BVH::Sampling_from_node, MC/BVH.h:114-129):
 //            1 x float4 per node (area, bits(left), bits(right), bits(light_tri)), root = 0
 //  ltris   : 4 x float4 per light triangle: (a, 0), (b, 0), (c, 0), (n, area)
+//  wmats   : Whitted-style shading (BVH Ray Tracer, BV/Renderer.cpp:172-229): 1 x float4 per
+//            material: (diffuse color, phong_diffuse)
+//  plights : point lights in insertion order (BV/LightSource.h, BV/Renderer.cpp:38-39):
+//            2 x float4 per light: (position, 0), (radiance, 0)
 #ifndef RT_LAYOUT_H
 #define RT_LAYOUT_H
 #include <stdint.h>
@@ -36,6 +40,8 @@ typedef struct {
     float light_area;          // light mesh BVH root mesh_area (pdf = 1/area, MC/BVH.h:106)
     float light_emission[3];   // emission of the light mesh material (MC/TriangleMesh.h:195)
     uint32_t max_depth;        // deepest node level (for diagnostics)
+    uint32_t n_plights;        // point lights (Whitted shading)
+    float sky[3];              // Whitted miss color (BV/Renderer.h:189)
 } rt_scene_header;
 
 #endif

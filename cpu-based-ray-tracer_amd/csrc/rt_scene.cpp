@@ -236,7 +236,12 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             F3 v[3];
             for (int j = 0; j < 3; ++j) {
                 const float* q = &raw[9 * t + 3 * j];
-                v[j] = F3{0.01f * q[0], 0.01f * q[1], 0.01f * q[2]};   // mesh_scale * vec3
+                const float sc = meshes_[mi].scale;
+                v[j] = F3{sc * q[0], sc * q[1], sc * q[2]};   // mesh_scale * vec3
+                if (meshes_[mi].has_offset) {                  // world_coordinates + mesh_scale * vec3
+                    const F3& o = meshes_[mi].offset;
+                    v[j] = F3{o.x + v[j].x, o.y + v[j].y, o.z + v[j].z};
+                }
                 rmin = F3{std::min(rmin.x, v[j].x), std::min(rmin.y, v[j].y), std::min(rmin.z, v[j].z)};
                 rmax = F3{std::max(rmax.x, v[j].x), std::max(rmax.y, v[j].y), std::max(rmax.z, v[j].z)};
             }
@@ -352,6 +357,21 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         q[0] = m.albedo.x / PI; q[1] = m.albedo.y / PI; q[2] = m.albedo.z / PI; q[3] = emitting ? 1.0f : 0.0f;
         q[4] = m.emission.x; q[5] = m.emission.y; q[6] = m.emission.z; q[7] = 0.0f;
     }
+    // ---- Whitted shading data: (diffuse color, phong_diffuse) per material; point lights; sky
+    out.wmats.resize(nm * 4);
+    for (size_t mi = 0; mi < nm; ++mi) {
+        const MaterialDesc& m = meshes_[mi].material;
+        float* q = &out.wmats[4 * mi];
+        q[0] = m.albedo.x; q[1] = m.albedo.y; q[2] = m.albedo.z; q[3] = m.phong_diffuse;
+    }
+    out.plights.resize(lights_.size() * 8);
+    for (size_t k = 0; k < lights_.size(); ++k) {
+        float* q = &out.plights[8 * k];
+        q[0] = lights_[k].position.x; q[1] = lights_[k].position.y; q[2] = lights_[k].position.z; q[3] = 0.0f;
+        q[4] = lights_[k].radiance.x; q[5] = lights_[k].radiance.y; q[6] = lights_[k].radiance.z; q[7] = 0.0f;
+    }
+    out.hdr.n_plights = (uint32_t)lights_.size();
+    out.hdr.sky[0] = sky_.x; out.hdr.sky[1] = sky_.y; out.hdr.sky[2] = sky_.z;
     // ---- light sampling tree: the light mesh's own BVH (BVH::Sampling_from_root)
     out.hdr.light_mesh = light;
     if (light >= 0) {

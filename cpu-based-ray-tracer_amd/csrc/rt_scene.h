@@ -12,18 +12,26 @@ namespace rt {
 
 struct F3 { float x, y, z; };
 
-struct MaterialDesc { F3 albedo; F3 emission; };
+// albedo: MC diffuse_coefficient (path tracing) / BV diffuse color (Whitted); phong_diffuse: BV only
+struct MaterialDesc { F3 albedo; F3 emission; float phong_diffuse = 0.0f; };
 
 struct MeshDesc {
-    std::vector<float> raw;   // de-indexed objl positions, 9 floats per triangle, BEFORE the 0.01 scale
+    std::vector<float> raw;   // de-indexed objl positions, 9 floats per triangle, BEFORE the scale
     MaterialDesc material;
     std::string name;
+    // vertex = scale * p (MC/TriangleMesh.h:165-168, scale 0.01), or with an offset
+    // vertex = offset + scale * p (BV/TriangleMesh.h:124-127)
+    float scale = 0.01f;
+    bool has_offset = false;
+    F3 offset{0.0f, 0.0f, 0.0f};
 };
+
+struct PointLight { F3 position; F3 radiance; };
 
 // Flattened, upload-ready scene (rt_layout.h).
 struct FlatScene {
     rt_scene_header hdr{};
-    std::vector<float> nodes, tris, mats, lnodes, ltris;   // float4-granular
+    std::vector<float> nodes, tris, mats, lnodes, ltris, wmats, plights;   // float4-granular
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag
     std::vector<float> dbg_node_f;    // 7 per node
     std::vector<int32_t> dbg_node_i;  // 5 per node
@@ -40,6 +48,9 @@ public:
     void add_cornell_box();
     static std::vector<MeshDesc> cornell_box_meshes();
     int add_mesh(MeshDesc m);
+    // Renderer::Add(std::unique_ptr<PointLightSource>), BV/Renderer.h:88-97
+    void add_point_light(const PointLight& l) { lights_.push_back(l); }
+    void set_sky(const F3& c) { sky_ = c; }
     // Renderer::GenerateBVH (MC/Renderer.h:83-86) + TriangleMesh's per-mesh BVH (MC/TriangleMesh.h:185)
     bool build(FlatScene& out, std::string& err) const;
     size_t num_meshes() const { return meshes_.size(); }
@@ -47,6 +58,8 @@ public:
 
 private:
     std::vector<MeshDesc> meshes_;
+    std::vector<PointLight> lights_;
+    F3 sky_{0.2f, 0.7f, 0.8f};   // BV/Renderer.h:189
 };
 
 }  // namespace rt

@@ -16,6 +16,8 @@
  *   rt_render                             Renderer::Render x n_frames (+ RayGen_Shader)     MC/Renderer.cpp:91-134
  *   rt_reset_accumulation                 Renderer::Reaccumulate                            MC/Renderer.h:57-60
  *   rt_trace                              Renderer::ray_BVH_intersection_record             MC/Renderer.h:88-91
+ *   rt_render + RT_RENDER_WHITTED         BVH Ray Tracer Renderer::Render / cast_Whitted_ray   BV/Renderer.cpp:69-233
+ *   rt_scene_add_bvh_tracer_scene         BVH Ray Tracer Renderer::Renderer()                  BV/Renderer.cpp:26-43
  */
 #ifndef RT_CAPI_H
 #define RT_CAPI_H
@@ -48,6 +50,20 @@ rt_status rt_scene_add_obj(rt_scene* s, const char* path, const float albedo[3],
 /* a TriangleMesh from de-indexed raw positions (9 floats per triangle, pre-scale, objl order) */
 rt_status rt_scene_add_mesh(rt_scene* s, const float* raw_positions, uint64_t n_tris, const float albedo[3], const float emission[3],
                             int32_t* mesh_id);
+/* Whitted-style scenes (the reference's "BVH Ray Tracer", BV/ = BVH Ray Tracer/8599RayTracerGUI/src/):
+ * a TriangleMesh(file, mesh_scale, world_coordinates) (BV/TriangleMesh.h:113-151): vertex =
+ * offset + scale * p (offset may be NULL: vertex = scale * p); every triangle Diffuse_Glossy with the
+ * given diffuse color and phong_diffuse (BV/TriangleMesh.h:64-67,138-141) */
+rt_status rt_scene_add_whitted_mesh(rt_scene* s, const float* raw_positions, uint64_t n_tris, float scale, const float offset[3],
+                                    const float diffuse[3], float phong_diffuse, int32_t* mesh_id);
+rt_status rt_scene_add_whitted_obj(rt_scene* s, const char* path, float scale, const float offset[3], const float diffuse[3],
+                                   float phong_diffuse, int32_t* mesh_id);
+/* Renderer::Add(std::unique_ptr<PointLightSource>) (BV/Renderer.h:88-97, BV/LightSource.h) */
+rt_status rt_scene_add_point_light(rt_scene* s, const float position[3], const float radiance[3]);
+/* Whitted miss color (default (0.2, 0.7, 0.8), BV/Renderer.h:189) */
+rt_status rt_scene_set_sky(rt_scene* s, const float rgb[3]);
+/* the BVH Ray Tracer's Renderer::Renderer() scene (BV/Renderer.cpp:26-43) from the two OBJ files */
+rt_status rt_scene_add_bvh_tracer_scene(rt_scene* s, const char* bunny_obj, const char* teapot_obj);
 rt_status rt_scene_build(rt_scene* s);
 
 typedef struct {
@@ -94,6 +110,8 @@ uint32_t rt_local_rows(const rt_ctx* ctx);
 #define RT_RENDER_COUNT 2u /* collect node/triangle/ray counters (rt_get_stats) */
 #define RT_RENDER_GLOBAL_SCENE 4u /* read the scene from HBM even when it fits in LDS (A/B) */
 #define RT_RENDER_GLOBAL_STACK 8u /* keep the whole EXACT fold stack in HBM (A/B) */
+#define RT_RENDER_WHITTED 16u /* Whitted-style shading with point lights and corner-of-pixel rays
+                                 (BV/Renderer.cpp:109-233) instead of Monte Carlo path tracing; seed/rr unused */
 typedef struct {
     uint32_t first_frame; /* 1-based frame index of the first sample (== reference frame_accumulating) */
     uint32_t n_frames;    /* samples per pixel rendered by this call */
@@ -124,6 +142,9 @@ typedef struct {
     uint32_t grid, block, stack_depth;
     /* RT_RENDER_COUNT scheduling diagnostics: wave-level executions */
     uint64_t wave_rounds, wave_steps, wave_tri_tests, wave_service;
+    /* RT_RENDER_COUNT: wave-level fold iterations; wave cycles (s_memtime) spent in service,
+     * work-queue + camera-ray, and traversal rounds; lanes served per service round (sum) */
+    uint64_t wave_fold, cycles_service, cycles_queue, cycles_trace, service_lanes;
 } rt_stats;
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 

@@ -7,6 +7,7 @@ inputs + outputs as small .npz fixtures.  Only data is stored: no reference sour
 Container-only (needs /root/reference); the GPU box uses the committed fixtures.
 
     python oracle/gen_golden.py            # all fixtures
+    python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
 """
 import os
 import subprocess
@@ -235,21 +236,132 @@ def gen_images():
     np.savez_compressed(os.path.join(GOLDEN, "images_cornell.npz"), **out)
 
 
+# ------------------------------------------------------------------ BVH Ray Tracer (config C3)
+BV_DIR = os.path.join(REF, "BVH Ray Tracer", "8599RayTracerGUI", "src")
+HARNESS_BV = os.path.join(HERE, "_ref", "ref_whitted_bvh")
+BV_NODE_FIELDS = ("mn", "mx", "left", "right", "tri", "mesh", "top")   # area: not part of the BV build
+
+
+def run_bv(*args):
+    r = subprocess.run([HARNESS_BV] + [str(a) for a in args], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"ref_whitted_bvh {args[0]} failed: {r.returncode} {r.stderr}")
+    print(" ", r.stdout.strip())
+
+
+def bv_objs():
+    return os.path.join(BV_DIR, "stanford_bunny.obj"), os.path.join(BV_DIR, "utah_teapot.obj")
+
+
+def scene_digest(nodes, tris):
+    """SHA-256 over the flattened topology and geometry (the fields both builds define)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in BV_NODE_FIELDS:
+        h.update(np.ascontiguousarray(nodes[f]).tobytes())
+    for f in ("a", "b", "c", "n", "mesh"):
+        h.update(np.ascontiguousarray(tris[f]).tobytes())
+    return h.hexdigest()
+
+
+def gen_bvh_scene():
+    bunny, teapot = bv_objs()
+    raw = {}
+    for name, path in (("bunny", bunny), ("teapot", teapot)):
+        run("objraw", path, tmp(name + ".raw"))
+        raw[name] = np.fromfile(tmp(name + ".raw"), "<f4").reshape(-1, 9)
+    run_bv("scene", bunny, teapot, tmp("bv_nodes"), tmp("bv_tris"))
+    nodes = np.fromfile(tmp("bv_nodes"), NODE_DT)
+    tris = np.fromfile(tmp("bv_tris"), TRI_DT)
+    np.savez_compressed(os.path.join(GOLDEN, "bvh_scene.npz"), raw_bunny=raw["bunny"], raw_teapot=raw["teapot"],
+                        n_nodes=np.int64(len(nodes)), n_tris=np.int64(len(tris)), digest=np.array(scene_digest(nodes, tris)),
+                        nodes_head=nodes[:512].view(np.uint8), tris_head=tris[:256].view(np.uint8))
+    return nodes, tris
+
+
+def gen_bvh_rays(nodes, tris, rng):
+    n = 4096
+    cam = np.array([-1, 5, 10], np.float32)
+    lo, hi = nodes["mn"][0], nodes["mx"][0]
+    o, d = [], []
+    k = 1500   # camera rays at the objects
+    tgt = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    o.append(np.repeat(cam[None], k, 0)); d.append(tgt - cam)
+    k = 1000   # random origins around the objects
+    o.append(rng.uniform(lo - 2, hi + 2, (k, 3)).astype(np.float32)); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    k = 500    # towards the point lights from surface-ish points (shadow rays)
+    ti = rng.integers(0, len(tris), k)
+    src = ((tris["a"][ti] + tris["b"][ti] + tris["c"][ti]) / 3).astype(np.float32)
+    light = np.where((rng.random(k) < 0.5)[:, None], np.array([-20, 70, 20], np.float32), np.array([20, 70, 20], np.float32))
+    o.append(src); d.append((light - src).astype(np.float32))
+    k = 300    # axis-aligned directions
+    oo = rng.uniform(lo - 1, hi + 1, (k, 3)).astype(np.float32)
+    dd = np.zeros((k, 3), np.float32)
+    dd[np.arange(k), rng.integers(0, 3, k)] = rng.choice([-1.0, 1.0], k)
+    o.append(oo); d.append(dd)
+    k = n - sum(len(x) for x in o)   # through vertices and edge midpoints (shared edges, ties)
+    ti = rng.integers(0, len(tris), k)
+    w = rng.integers(0, 3, k)
+    a, b, c = tris["a"][ti], tris["b"][ti], tris["c"][ti]
+    tgt = np.where((w == 0)[:, None], a, np.where((w == 1)[:, None], 0.5 * (a + b), 0.5 * (b + c)))
+    o.append(np.repeat(cam[None], k, 0)); d.append((tgt - cam).astype(np.float32))
+    o = np.concatenate(o).astype(np.float32)
+    d = np.concatenate(d).astype(np.float32)
+    np.concatenate([o, d], 1).astype("<f4").tofile(tmp("bv_rays.in"))
+    bunny, teapot = bv_objs()
+    run_bv("rays", bunny, teapot, tmp("bv_rays.in"), tmp("bv_rays.out"))
+    res = np.fromfile(tmp("bv_rays.out"), HIT_DT)
+    np.savez_compressed(os.path.join(GOLDEN, "bvh_rays.npz"), org=o, dir=d, hit=res["hit"], tri=res["tri"], t=res["t"],
+                        loc=res["loc"], n=res["n"])
+
+
+def gen_bvh_images():
+    import hashlib
+    bunny, teapot = bv_objs()
+    out = {}
+    for (W, H) in [(16, 12), (1280, 960)]:
+        run_bv("camera", W, H, tmp("bv_cam"))
+        b = np.fromfile(tmp("bv_cam"), np.uint8)
+        out[f"mats_{W}x{H}"] = b[:256].view("<f4").reshape(4, 4, 4)
+        out[f"vec_{W}x{H}"] = b[256:280].view("<f4")
+        if W * H <= 4096:
+            out[f"dirs_{W}x{H}"] = b[280:].view("<f4").reshape(-1, 3)
+    for (W, H, spp) in [(160, 120, 3), (97, 61, 2), (1280, 960, 64)]:
+        run_bv("image", bunny, teapot, W, H, spp, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        key = f"{W}x{H}_spp{spp}"
+        if W * H <= 20000:
+            out[f"accum_{key}"] = acc
+            out[f"rgba_{key}"] = rgba
+        out[f"sha_accum_{key}"] = np.array(hashlib.sha256(acc.tobytes()).hexdigest())
+        out[f"sha_rgba_{key}"] = np.array(hashlib.sha256(rgba.tobytes()).hexdigest())
+        out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
+    np.savez_compressed(os.path.join(GOLDEN, "bvh_images.npz"), **out)
+
+
 def main():
     global TMP
-    if not os.path.exists(HARNESS):
+    if not os.path.exists(HARNESS) or not os.path.exists(HARNESS_BV):
         subprocess.check_call(["make", "-C", HERE, "ref"])
     os.makedirs(GOLDEN, exist_ok=True)
-    rng = np.random.default_rng(20260101)
+    only = sys.argv[1] if len(sys.argv) > 1 else "all"
     with tempfile.TemporaryDirectory() as TMP:
-        tris = gen_scene()
-        gen_rays(tris, rng)
-        gen_mt(rng)
-        gen_aabb(rng)
-        gen_light(rng)
-        gen_material(rng)
-        gen_camera()
-        gen_images()
+        if only in ("all", "cornell"):
+            rng = np.random.default_rng(20260101)
+            tris = gen_scene()
+            gen_rays(tris, rng)
+            gen_mt(rng)
+            gen_aabb(rng)
+            gen_light(rng)
+            gen_material(rng)
+            gen_camera()
+            gen_images()
+        if only in ("all", "bvh"):
+            rng = np.random.default_rng(20261015)
+            nodes, tris = gen_bvh_scene()
+            gen_bvh_rays(nodes, tris, rng)
+            gen_bvh_images()
     print("golden fixtures written to", GOLDEN)
 
 

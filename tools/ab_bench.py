@@ -59,7 +59,13 @@ def main():
                           grid=st.grid, step_lane_eff=st.node_tests / max(1, 64 * st.wave_steps),
                           mt_lane_eff=st.tri_tests / max(1, 64 * st.wave_tri_tests),
                           wave_steps_per_sample=st.wave_steps / st.samples, wave_mt_per_sample=st.wave_tri_tests / st.samples,
-                          wave_rounds_per_sample=st.wave_rounds / st.samples, wave_service_per_sample=st.wave_service / st.samples)
+                          wave_rounds_per_sample=st.wave_rounds / st.samples, wave_service_per_sample=st.wave_service / st.samples,
+                          wave_fold_per_sample=st.wave_fold / st.samples,
+                          service_lane_eff=st.service_lanes / max(1, 64 * st.wave_service))
+            cyc = st.cycles_service + st.cycles_queue + st.cycles_trace
+            out[n].update(cycle_share={"service": st.cycles_service / cyc, "queue_camera": st.cycles_queue / cyc,
+                                       "trace": st.cycles_trace / cyc},
+                          wave_cycles_per_sample=cyc / st.samples)
     base = images[names[0]].view(np.uint32)
     for n in names[1:]:
         out[n]["bitwise_equal_to_" + names[0]] = bool(np.array_equal(images[n].view(np.uint32), base))
