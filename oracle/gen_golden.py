@@ -8,6 +8,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
 
     python oracle/gen_golden.py            # all fixtures
     python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
+    python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
 """
 import os
 import subprocess
@@ -236,6 +237,16 @@ def gen_images():
     np.savez_compressed(os.path.join(GOLDEN, "images_cornell.npz"), **out)
 
 
+def gen_stat():
+    """The reference with its SHIPPED random stream (serial std::mt19937 seeded 5489, MSVC 32-bit
+    distribution, camera draws then pixel loop per frame): the statistical gate of SURVEY.md 8(d)."""
+    W, H, spp, rr = 64, 64, 1024, 0.8
+    run("image_mt", CORNELL_DIR, W, H, spp, rr, tmp("mt_acc"))
+    acc = np.fromfile(tmp("mt_acc"), "<f4").reshape(H, W, 4)
+    np.savez_compressed(os.path.join(GOLDEN, "stat_mt19937.npz"), accum=acc, W=np.int64(W), H=np.int64(H), spp=np.int64(spp),
+                        rr=np.float32(rr))
+
+
 # ------------------------------------------------------------------ BVH Ray Tracer (config C3)
 BV_DIR = os.path.join(REF, "BVH Ray Tracer", "8599RayTracerGUI", "src")
 HARNESS_BV = os.path.join(HERE, "_ref", "ref_whitted_bvh")
@@ -357,6 +368,8 @@ def main():
             gen_material(rng)
             gen_camera()
             gen_images()
+        if only in ("all", "cornell", "stat"):
+            gen_stat()
         if only in ("all", "bvh"):
             rng = np.random.default_rng(20261015)
             nodes, tris = gen_bvh_scene()

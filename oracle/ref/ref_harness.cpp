@@ -534,6 +534,37 @@ static int cmd_image(const char* dir, const char* extra, uint32_t W, uint32_t H,
     return overflow ? 5 : 0;
 }
 
+// The SHIPPED random stream, serially (statistical gate): one persistent
+// thread_local std::mt19937 default-seeded with 5489 (WN/Random.cpp:5), the MSVC 32-bit distribution,
+// and the reference's draw order per frame: Camera::RecomputeRayDirections draws 2 uniforms per
+// pixel y-major (MC/Camera.cpp:114-132, via UpdateCamera before Render, MC/mainloop.cpp:32-41), then
+// Render's pixel loop runs y-major (serial under libstdc++ without TBB, MC/Renderer.cpp:100-110).
+// No injection: this is the reference's own sequence, for the statistical comparison only.
+static int cmd_image_mt(const char* dir, uint32_t W, uint32_t H, uint32_t spp, float rr, const char* out_accum)
+{
+    Scene* s = build_cornell(dir, {});
+    Camera cam{35.0f, 0.1f, 100.0f};
+    cam.ResizeViewport(W, H);
+    Walnut::Random::s_RandomEngine.seed(5489u);
+    set_msvc_distribution();
+    Hybrid h{s, rr};
+    std::vector<glm::vec4> acc((size_t)W * H, glm::vec4(0.0f));
+    std::vector<glm::vec3> dirs((size_t)W * H);
+    for (uint32_t f = 1; f <= spp; ++f) {
+        for (uint32_t y = 0; y < H; ++y)
+            for (uint32_t x = 0; x < W; ++x) dirs[(size_t)y * W + x] = camera_dir(cam, x, y, W, H);
+        for (uint32_t y = 0; y < H; ++y)
+            for (uint32_t x = 0; x < W; ++x) {
+                const size_t px = (size_t)y * W + x;
+                acc[px] += glm::vec4{h.cast_path(AccelerationStructure::Ray{cam.Position(), Whitted::normalize(dirs[px])}), 1.0f};
+            }
+    }
+    Out o(out_accum);
+    fwrite(acc.data(), 16, acc.size(), o.f);
+    printf("image_mt %ux%u spp %u\n", W, H, spp);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     check_layout_once();
@@ -548,6 +579,8 @@ int main(int argc, char** argv)
     if (c == "light" && argc == 5) return cmd_light(argv[2], argv[3], argv[4]);
     if (c == "material" && argc == 4) return cmd_material(argv[2], argv[3]);
     if (c == "camera" && argc == 7) return cmd_camera(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), strtoull(argv[5], 0, 10), argv[6]);
+    if (c == "image_mt" && argc == 8)
+        return cmd_image_mt(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), (float)atof(argv[6]), argv[7]);
     if (c == "image" && argc == 13)
         return cmd_image(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), strtoull(argv[7], 0, 10), (float)atof(argv[8]), atoi(argv[9]),
                          argv[10], argv[11], argv[12]);
