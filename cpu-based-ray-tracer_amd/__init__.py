@@ -131,6 +131,11 @@ class Scene:
         s.build()
         return s
 
+    @classmethod
+    def cornell_c5(cls, bunny_raw):
+        """Configuration C5: the Cornell box plus the synthesized 79,488-triangle bunny (c5_mesh)."""
+        return cls.cornell(extra=[(c5_mesh(bunny_raw), (0.7, 0.7, 0.7), (0.0, 0.0, 0.0))])
+
     def add_mesh(self, raw, albedo, emission):
         raw = np.ascontiguousarray(raw, np.float32).reshape(-1, 9)
         mid = C.c_int32()
@@ -194,6 +199,51 @@ class Scene:
                 self.h = C.c_void_p()
         except Exception:
             pass
+
+
+def subdivide_midpoint(raw, levels=1):
+    """1:4 midpoint subdivision of a de-indexed triangle list (n, 9) float32, `levels` times.
+
+    Each (a, b, c) becomes (a, ab, ca), (ab, b, bc), (ca, bc, c), (ab, bc, ca) with the float32
+    midpoints m = (p + q) * 0.5 (commutative, so triangles sharing an edge share its midpoint and the
+    mesh stays watertight); orientation is kept.  Used to synthesize the ~80k-triangle mesh of the C5
+    configuration (SURVEY.md section 7 'Config 5', 8(d))."""
+    t = np.ascontiguousarray(raw, np.float32).reshape(-1, 3, 3)
+    half = np.float32(0.5)
+    for _ in range(levels):
+        a, b, c = t[:, 0], t[:, 1], t[:, 2]
+        ab, bc, ca = (a + b) * half, (b + c) * half, (c + a) * half
+        t = np.stack([np.stack([a, ab, ca], 1), np.stack([ab, b, bc], 1), np.stack([ca, bc, c], 1), np.stack([ab, bc, ca], 1)], 1)
+        t = np.ascontiguousarray(t.reshape(-1, 3, 3), np.float32)
+    return t.reshape(-1, 9)
+
+
+def fit_mesh(raw, height, base_center, obj_units=100.0):
+    """Uniformly scale a triangle list to `height` with its bounding-box bottom centre at `base_center`
+    (world units), returned in OBJ units (world x `obj_units`) so that the reference's fixed 0.01 mesh
+    scale (MC/TriangleMesh.h:150,170) restores world units.  float32 throughout, fixed operation order."""
+    v = np.ascontiguousarray(raw, np.float32).reshape(-1, 3)
+    lo, hi = v.min(0), v.max(0)
+    s = np.float32(height) / (hi[1] - lo[1])
+    anchor = np.array([(lo[0] + hi[0]) * np.float32(0.5), lo[1], (lo[2] + hi[2]) * np.float32(0.5)], np.float32)
+    w = (v - anchor) * s + np.asarray(base_center, np.float32)
+    return np.ascontiguousarray((w * np.float32(obj_units)).reshape(-1, 9), np.float32)
+
+
+def c5_mesh(bunny_raw):
+    """The C5 asset: the Stanford bunny (raw objl positions) subdivided 1:4 twice
+    (4,968 -> 79,488 triangles), 1.5 units tall, standing on the floor (y = 0) at x = 4.2, z = 1.2,
+    clear of both boxes; white albedo 0.7 (added to the Cornell scene via Add + GenerateBVH,
+    MC/Renderer.h:78-86)."""
+    return fit_mesh(subdivide_midpoint(bunny_raw, 2), 1.5, (4.2, 0.0, 1.2))
+
+
+def write_obj(path, raw):
+    """De-indexed triangle list -> OBJ text whose values round-trip exactly through std::stof."""
+    v = np.ascontiguousarray(raw, np.float32).reshape(-1, 3)
+    with open(path, "w") as f:
+        f.write("".join("v %.9g %.9g %.9g\n" % (x, y, z) for x, y, z in v.astype(np.float64)))
+        f.write("".join("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3) for i in range(v.shape[0] // 3)))
 
 
 def camera_look(W, H, position, forward, vfov=35.0, near=0.1, far=100.0):

@@ -8,6 +8,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
 
     python oracle/gen_golden.py            # all fixtures
     python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
+    python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
 """
 import os
@@ -351,6 +352,73 @@ def gen_bvh_images():
     np.savez_compressed(os.path.join(GOLDEN, "bvh_images.npz"), **out)
 
 
+# ------------------------------------------------------------------ Cornell box + synthesized mesh (config C5)
+def load_pkg():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(REPO, "cpu-based-ray-tracer_amd", "__init__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def gen_c5(rng):
+    """C5: the Cornell box + the 79,488-triangle subdivided bunny, added through the reference's own
+    TriangleMesh(OBJ, white) + BVH (build_cornell's `extra`).  The OBJ is generated from the committed
+    raw bunny (bvh_scene.npz) by the package's c5_mesh(); its values round-trip exactly through stof."""
+    import hashlib
+    rt = load_pkg()
+    bunny = np.load(os.path.join(GOLDEN, "bvh_scene.npz"))["raw_bunny"]
+    raw = rt.c5_mesh(bunny)
+    obj = tmp("c5_bunny.obj")
+    rt.write_obj(obj, raw)
+    run("objraw", obj, tmp("c5.raw"))
+    assert np.array_equal(np.fromfile(tmp("c5.raw"), "<f4").reshape(-1, 9).view(np.uint32), raw.view(np.uint32))
+    run("scene", CORNELL_DIR, obj, tmp("c5_nodes"), tmp("c5_tris"), tmp("c5_meshes"))
+    nodes = np.fromfile(tmp("c5_nodes"), NODE_DT)
+    tris = np.fromfile(tmp("c5_tris"), TRI_DT)
+    out = dict(n_nodes=np.int64(len(nodes)), n_tris=np.int64(len(tris)), digest=np.array(scene_digest(nodes, tris)),
+               nodes_head=nodes[:512].view(np.uint8), tris_head=tris[:256].view(np.uint8),
+               raw_sha=np.array(hashlib.sha256(raw.tobytes()).hexdigest()))
+    # closest-hit rays: camera rays at the bunny, interior rays, rays grazing bunny vertices/edges
+    n = 4096
+    cam = np.array([2.81432, 4.20749, -9.11751], np.float32)
+    lo, hi = raw.reshape(-1, 3).min(0) * np.float32(0.01), raw.reshape(-1, 3).max(0) * np.float32(0.01)
+    o, d = [], []
+    k = 1500
+    o.append(np.repeat(cam[None], k, 0)); d.append(rng.uniform(lo, hi, (k, 3)).astype(np.float32) - cam)
+    k = 1500
+    room_lo, room_hi = np.array([0, 0, 0], np.float32), np.array([5.56, 5.488, 5.592], np.float32)
+    o.append(rng.uniform(room_lo, room_hi, (k, 3)).astype(np.float32)); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    k = n - 3000
+    bt = tris[tris["mesh"] == 6]
+    ti = rng.integers(0, len(bt), k)
+    w = rng.integers(0, 3, k)
+    a, b, c = bt["a"][ti], bt["b"][ti], bt["c"][ti]
+    tgt = np.where((w == 0)[:, None], a, np.where((w == 1)[:, None], 0.5 * (a + b), (a + b + c) / 3)).astype(np.float32)
+    src = rng.uniform(room_lo, room_hi, (k, 3)).astype(np.float32)
+    o.append(src); d.append((tgt - src).astype(np.float32))
+    o = np.concatenate(o).astype(np.float32)
+    d = np.concatenate(d).astype(np.float32)
+    np.concatenate([o, d], 1).astype("<f4").tofile(tmp("c5_rays.in"))
+    run("rays", CORNELL_DIR, obj, tmp("c5_rays.in"), tmp("c5_rays.out"))
+    res = np.fromfile(tmp("c5_rays.out"), HIT_DT)
+    out.update(ray_org=o, ray_dir=d, ray_hit=res["hit"], ray_tri=res["tri"], ray_t=res["t"])
+    # images: a small one stored whole, the full C5 frame (3840x2160) at 1 spp by SHA-256, and the
+    # per-sample work counters at 480x270 (SURVEY.md 8(d) table)
+    for (W, H, spp, seed) in [(96, 54, 16, 0), (3840, 2160, 1, 0), (480, 270, 4, 3)]:
+        run("image", CORNELL_DIR, obj, W, H, spp, seed, 0.8, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        key = f"{W}x{H}_spp{spp}_s{seed}"
+        if W * H <= 20000:
+            out[f"accum_{key}"] = acc
+            out[f"rgba_{key}"] = rgba
+        out[f"sha_accum_{key}"] = np.array(hashlib.sha256(acc.tobytes()).hexdigest())
+        out[f"sha_rgba_{key}"] = np.array(hashlib.sha256(rgba.tobytes()).hexdigest())
+        out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
+    np.savez_compressed(os.path.join(GOLDEN, "c5_scene.npz"), **out)
+
+
 def main():
     global TMP
     if not os.path.exists(HARNESS) or not os.path.exists(HARNESS_BV):
@@ -375,6 +443,8 @@ def main():
             nodes, tris = gen_bvh_scene()
             gen_bvh_rays(nodes, tris, rng)
             gen_bvh_images()
+        if only in ("all", "c5"):
+            gen_c5(np.random.default_rng(20261016))
     print("golden fixtures written to", GOLDEN)
 
 

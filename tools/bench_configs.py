@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Per-configuration throughput on ONE MI355X.
+
+bench.py reports the headline (C4); this prints one JSON line per configuration with the megakernel
+time (HIP events on its stream), Msamples/s, and the algorithmic-bytes roofline of SURVEY.md 8(d)
+(reference work per sample x measured samples/s vs 8 TB/s).  C5 runs at a reduced spp (frames are
+i.i.d. and the kernel time is linear in spp); the spp used is in each line.
+
+    python tools/bench_configs.py                 # all configs
+    python tools/bench_configs.py --configs C5 --c5-spp 64
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from _rt import rt  # noqa: E402
+
+HBM_PEAK = 8000.0
+# reference work per sample, SURVEY.md 8(d): rays/sample, node tests/ray, triangle tests/ray
+WORK = {"C2": (5.700, 27.84, 4.06), "C3": (1.446, 38.26, 2.57), "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
+
+
+def bytes_per_sample(c):
+    r, n, t = WORK[c]
+    return r * (n * 32 + t * 36 + 16)
+
+
+def run(ctx, cam, W, H, spp, reps, **kw):
+    ctx.resize(W, H)
+    ctx.render(cam, min(spp, 8), fetch=False, **kw)   # warm-up
+    ms = []
+    for _ in range(reps):
+        ctx.render(cam, spp, fetch=False, **kw)
+        ms.append(ctx.stats().last_kernel_ms)
+    return float(np.median(ms))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--c5-spp", type=int, default=64)
+    ap.add_argument("--fast", action="store_true")
+    args = ap.parse_args()
+    bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
+    for c in args.configs.split(","):
+        ctx = rt.Context(0)
+        kw = {}
+        if c in ("C2", "C4"):
+            ctx.upload(rt.Scene.cornell())
+            W, H, spp = (784, 784, 256) if c == "C2" else (1920, 1080, 1024)
+            cam, _, _ = rt.camera_default(W, H)
+            kw = dict(exact=not args.fast)
+        elif c == "C3":
+            ctx.upload(rt.Scene.bvh_tracer(bvh["raw_bunny"], bvh["raw_teapot"]))
+            W, H, spp = 1280, 960, 64
+            cam = rt.camera_bvh_tracer(W, H)
+            kw = dict(whitted=True)
+        elif c == "C5":
+            ctx.upload(rt.Scene.cornell_c5(bvh["raw_bunny"]))
+            W, H, spp = 3840, 2160, args.c5_spp
+            cam, _, _ = rt.camera_default(W, H)
+            kw = dict(exact=not args.fast)
+        else:
+            raise SystemExit(f"unknown config {c}")
+        ms = run(ctx, cam, W, H, spp, args.reps, **kw)
+        st = ctx.stats()
+        samples = W * H * spp
+        rate = samples / (ms / 1e3)
+        bps = bytes_per_sample(c)
+        print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
+                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid,
+                          "roofline": {"bytes_per_sample": round(bps, 1), "achieved_gbs": round(bps * rate / 1e9, 1),
+                                       "peak_gbs": HBM_PEAK, "frac": round(bps * rate / 1e9 / HBM_PEAK, 4)},
+                          "mode": "whitted" if c == "C3" else ("fast" if args.fast else "exact")}), flush=True)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
