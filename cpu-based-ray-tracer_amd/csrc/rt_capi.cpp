@@ -47,6 +47,7 @@ struct rt_ctx {
     rt_stats stats{};
     bool pending_stats = false;
     uint32_t last_flags = 0;
+    uint32_t variant = 0;
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
 
@@ -238,6 +239,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     c->device = cfg ? cfg->device : 0;
     if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = std::getenv("RT_VARIANT")) c->variant = (uint32_t)std::strtoul(e, nullptr, 10);
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
     if (cfg && cfg->stream) {
@@ -374,7 +376,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
-    P.thresh = c->thresh; P.steps = c->steps;
+    P.thresh = c->thresh; P.steps = c->steps; P.variant = c->variant;
     // small scenes are staged into LDS (one copy per workgroup)
     const size_t lds_bytes = rt_scene_lds_bytes(P);
     const bool lds = (p->flags & RT_RENDER_GLOBAL_SCENE) == 0 && lds_bytes <= kMaxLdsScene;
@@ -485,13 +487,16 @@ rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, in
     P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes; P.tris = c->d_tris;
     if ((e = hipMemcpyAsync(d_o, org, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess ||
         (e = rt_launch_trace(P, (uint32_t)n, d_o, d_d, d_tri, d_t, c->stream)) != hipSuccess ||
+        (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(tri, d_tri, n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipMemcpyAsync(t, d_t, n * 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         cleanup(); return hip_fail(c, e, "rt_trace");
     }
     cleanup();
+    c->pending_stats = true;   // last_kernel_ms = the trace kernel
     return RT_OK;
 }
 

@@ -33,6 +33,7 @@ struct KParams {
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
+    uint32_t variant;               // A/B of traversal-loop forms (RT_VARIANT; 0 = default)
 };
 
 // LDS staging of the scene: bytes needed (the kernel's dynamic shared memory when lds == true)

@@ -133,8 +133,11 @@ __device__ __forceinline__ V3 sample_hemisphere(V3 n, Rng& g)
 
 }  // namespace
 
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 1   // minimum waves per SIMD the register allocation must admit (A/B knob)
+#endif
 template <bool EXACT, bool COUNT, bool LDS>
-__global__ void __launch_bounds__(256) pt_megakernel(KParams P)
+__global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
     SceneView S;
@@ -425,7 +428,26 @@ __global__ void __launch_bounds__(256) pt_megakernel(KParams P)
             if (tracing) {
                 // box steps; up to two leaves are parked (in DFS order) before the lane stops
                 int parked0 = -1, parked1 = -1;
-                if (fin) {
+                if (fin && P.variant == 1) {
+                    // predicated form: no per-lane branches inside the loop; a lane whose walk ended or
+                    // which holds two parked leaves keeps its state (selects), the wave leaves the loop
+                    // when no lane is active
+                    for (uint32_t s = 0; s < P.steps; ++s) {
+                        const bool act = ti < NN && parked1 < 0;
+                        if (!__any(act)) break;
+                        const uint32_t idx = act ? ti : 0u;
+                        const float4 q0 = S.nodes[2 * idx];
+                        const float4 q1 = S.nodes[2 * idx + 1];
+                        if (COUNT) { if (act) ++node_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_steps; }
+                        const bool hit = slab_hit_finite(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                        const int tri = f2i(q1.w);
+                        const uint32_t nti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
+                        const bool leaf = act && hit && tri >= 0;
+                        ti = act ? nti : ti;
+                        parked1 = (leaf && parked0 >= 0) ? tri : parked1;
+                        parked0 = (leaf && parked0 < 0) ? tri : parked0;
+                    }
+                } else if (fin) {
                     for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
                         const float4 q0 = S.nodes[2 * ti];
                         const float4 q1 = S.nodes[2 * ti + 1];

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""A/B of whole library builds (e.g. different kernel compile flags) in ONE process, interleaved rounds.
+
+    make -C cpu-based-ray-tracer_amd LIB=librt_hip_lb5.so BUILD=build_lb5 KFLAGS=-DRT_MIN_WAVES=5 librt_hip_lb5.so
+    python tools/ab_libs.py librt_hip.so librt_hip_lb5.so --spp 64
+"""
+import argparse
+import importlib.util
+import json
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
+
+
+def load(libname):
+    spec = importlib.util.spec_from_file_location("rt_amd_" + libname.replace(".", "_"), os.path.join(PKG, "__init__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m.LIB_PATH = os.path.join(PKG, libname)
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--fast", action="store_true")
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    args = ap.parse_args()
+    W, H, spp = args.width, args.height, args.spp
+    runs = {}
+    for name in args.libs:
+        rt = load(name)
+        if args.scene == "c5":
+            sc = rt.Scene.cornell_c5(np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"])
+        else:
+            sc = rt.Scene.cornell()
+        ctx = rt.Context(0)
+        ctx.upload(sc)
+        ctx.resize(W, H)
+        cam, _, _ = rt.camera_default(W, H)
+        runs[name] = (rt, ctx, cam, [], sc)
+    ref = None
+    for r in range(args.rounds + 1):
+        for name, (rt, ctx, cam, res, _) in runs.items():
+            ctx.render(cam, spp, fetch=False, exact=not args.fast)
+            if r > 0:
+                res.append(W * H * spp / ctx.stats().last_kernel_ms / 1e3)
+    out = {}
+    for name, (rt, ctx, cam, res, _) in runs.items():
+        _, acc = ctx.render(cam, 4, exact=not args.fast)
+        same = None if ref is None else bool(np.array_equal(acc.view(np.uint32), ref.view(np.uint32)))
+        ref = acc if ref is None else ref
+        out[name] = {"median_msps": round(float(np.median(res)), 1), "grid": ctx.stats().grid, "bitwise_equal_to_first": same}
+        ctx.close()
+    print(json.dumps({"config": f"{W}x{H}x{spp} {args.scene} {'fast' if args.fast else 'exact'}", "libs": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
