@@ -51,6 +51,15 @@ class Stats(C.Structure):
                 ("service_lanes", C.c_uint64)]
 
 
+class WorldMaterial(C.Structure):
+    """rt_world_material: a Whitted Style Ray Tracer entity's material (WH/Entity.h:49-55)."""
+    _fields_ = [("nature", C.c_int32), ("refractive_index", C.c_float), ("phong_diffuse", C.c_float), ("phong_specular", C.c_float),
+                ("specular_size_factor", C.c_float), ("diffuse_color", C.c_float * 3)]
+
+
+REFLECTIVE, REFLECTIVE_REFRACTIVE, DIFFUSE_GLOSSY = 0, 1, 2
+
+
 class SceneInfo(C.Structure):
     _fields_ = [("n_meshes", C.c_uint32), ("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_light_tris", C.c_uint32),
                 ("max_depth", C.c_uint32), ("light_mesh", C.c_int32), ("light_area", C.c_float), ("device_bytes", C.c_uint64)]
@@ -100,6 +109,11 @@ def lib():
         "rt_get_stats": (i32, [vp, C.POINTER(Stats)]),
         "rt_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(C.c_double)]),
         "rt_math_selftest": (i32, [vp, u64, fp, fp]),
+        "rt_world_material_default": (None, [C.POINTER(WorldMaterial)]),
+        "rt_scene_add_world_sphere": (i32, [vp, fp, C.c_float, C.POINTER(WorldMaterial), C.POINTER(i32)]),
+        "rt_scene_add_world_mesh": (i32, [vp, fp, u32, C.POINTER(u32), u32, fp, C.POINTER(WorldMaterial), C.POINTER(i32)]),
+        "rt_scene_add_two_spheres_scene": (i32, [vp]),
+        "rt_world_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(i32), fp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -173,6 +187,43 @@ class Scene:
         s.add_whitted_mesh(teapot_raw, 1.0, (-1.0, 3.0, 0.0))
         s.add_point_light((-20.0, 70.0, 20.0))
         s.add_point_light((20.0, 70.0, 20.0))
+        return s.build()
+
+    # ---- the Whitted Style Ray Tracer's world (config C1, WH/Renderer.cpp:27-49)
+    @staticmethod
+    def world_material(nature=DIFFUSE_GLOSSY, **kw):
+        m = WorldMaterial()
+        lib().rt_world_material_default(C.byref(m))
+        m.nature = nature
+        for k, v in kw.items():
+            if k == "diffuse_color":
+                m.diffuse_color[:] = [float(c) for c in v]
+            else:
+                setattr(m, k, float(v))
+        return m
+
+    def add_world_sphere(self, center, radius, material=None):
+        mid = C.c_int32()
+        self._check(lib().rt_scene_add_world_sphere(self.h, _fp(np.asarray(center, np.float32)), float(radius),
+                                                    C.byref(material) if material is not None else None, C.byref(mid)),
+                    "rt_scene_add_world_sphere")
+        return mid.value
+
+    def add_world_mesh(self, vertices, indices, uv, material=None):
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 3)
+        i = np.ascontiguousarray(indices, np.uint32).reshape(-1, 3)
+        t = np.ascontiguousarray(uv, np.float32).reshape(-1, 2)
+        mid = C.c_int32()
+        self._check(lib().rt_scene_add_world_mesh(self.h, _fp(v), v.shape[0], i.ctypes.data_as(C.POINTER(C.c_uint32)), i.shape[0], _fp(t),
+                                                  C.byref(material) if material is not None else None, C.byref(mid)),
+                    "rt_scene_add_world_mesh")
+        return mid.value
+
+    @classmethod
+    def two_spheres(cls):
+        """The Whitted Style Ray Tracer's Renderer::Renderer() world (WH/Renderer.cpp:27-49)."""
+        s = cls()
+        s._check(lib().rt_scene_add_two_spheres_scene(s.h), "rt_scene_add_two_spheres_scene")
         return s.build()
 
     def build(self):
@@ -255,6 +306,11 @@ def camera_look(W, H, position, forward, vfov=35.0, near=0.1, far=100.0):
     return cam
 
 
+def camera_two_spheres(W, H):
+    """The Whitted Style Ray Tracer's Camera{35, 0.1, 100} at (0, 0, 6) looking down -z (WH/Camera.h:17-19, WH/mainloop.cpp:23)."""
+    return camera_look(W, H, (0.0, 0.0, 6.0), (0.0, 0.0, -1.0))
+
+
 def camera_bvh_tracer(W, H):
     """The BVH Ray Tracer's Camera{35, 0.1, 100} at (-1, 5, 10) looking down -z (BV/Camera.h:19-20, BV/mainloop.cpp:22)."""
     return camera_look(W, H, (-1.0, 5.0, 10.0), (0.0, 0.0, -1.0))
@@ -332,9 +388,17 @@ class Context:
                                    t.ctypes.data_as(C.POINTER(C.c_double))), "rt_trace")
         return tri, t
 
+    def world_trace(self, org, dirs):
+        org = np.ascontiguousarray(org, np.float32); dirs = np.ascontiguousarray(dirs, np.float32)
+        n = org.shape[0]
+        ent = np.zeros(n, np.int32); tri = np.zeros(n, np.int32); tb = np.zeros((n, 3), np.float32)
+        self._check(lib().rt_world_trace(self.h, n, _fp(org), _fp(dirs), ent.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         tri.ctypes.data_as(C.POINTER(C.c_int32)), _fp(tb)), "rt_world_trace")
+        return ent, tri, tb
+
     def math_selftest(self, x):
         x = np.ascontiguousarray(x, np.float32)
-        out = np.zeros((x.shape[0], 6), np.float32)
+        out = np.zeros((x.shape[0], 7), np.float32)
         self._check(lib().rt_math_selftest(self.h, x.shape[0], _fp(x), _fp(out)), "rt_math_selftest")
         return out
 

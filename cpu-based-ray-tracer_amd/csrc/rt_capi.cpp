@@ -27,7 +27,7 @@ struct rt_ctx {
     std::string err;
     // scene
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr;
-    float4 *d_wmats = nullptr, *d_plights = nullptr;
+    float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
     // image
@@ -194,6 +194,62 @@ rt_status rt_scene_add_bvh_tracer_scene(rt_scene* s, const char* bunny_obj, cons
     return RT_OK;
 }
 
+void rt_world_material_default(rt_world_material* m)
+{
+    if (!m) return;
+    const rt::WorldEntity d;
+    m->nature = d.nature; m->refractive_index = d.refractive_index; m->phong_diffuse = d.phong_diffuse;
+    m->phong_specular = d.phong_specular; m->specular_size_factor = d.specular_size_factor;
+    m->diffuse_color[0] = d.diffuse_color.x; m->diffuse_color[1] = d.diffuse_color.y; m->diffuse_color[2] = d.diffuse_color.z;
+}
+
+static bool world_material(rt::WorldEntity& e, const rt_world_material* m)
+{
+    if (!m) return true;   // WH/Entity.h defaults
+    if (m->nature < 0 || m->nature > 2) return false;
+    e.nature = m->nature; e.refractive_index = m->refractive_index; e.phong_diffuse = m->phong_diffuse;
+    e.phong_specular = m->phong_specular; e.specular_size_factor = m->specular_size_factor;
+    e.diffuse_color = rt::F3{m->diffuse_color[0], m->diffuse_color[1], m->diffuse_color[2]};
+    return true;
+}
+
+rt_status rt_scene_add_world_sphere(rt_scene* s, const float center[3], float radius, const rt_world_material* m, int32_t* entity_id)
+{
+    if (!s || !center || !(radius > 0.0f)) return RT_ERR_INVALID;
+    rt::WorldEntity e;
+    e.kind = 0; e.center = rt::F3{center[0], center[1], center[2]}; e.radius = radius;
+    if (!world_material(e, m)) return RT_ERR_INVALID;
+    const int id = s->builder.add_world_entity(std::move(e));
+    if (entity_id) *entity_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_world_mesh(rt_scene* s, const float* vertices, uint32_t n_vertices, const uint32_t* indices, uint32_t n_tris,
+                                  const float* uv, const rt_world_material* m, int32_t* entity_id)
+{
+    if (!s || !vertices || !indices || !uv || n_vertices == 0 || n_tris == 0) return RT_ERR_INVALID;
+    rt::WorldEntity e;
+    e.kind = 1;
+    for (uint32_t i = 0; i < n_vertices; ++i) e.vertices.push_back(rt::F3{vertices[3 * i], vertices[3 * i + 1], vertices[3 * i + 2]});
+    e.indices.assign(indices, indices + 3 * (size_t)n_tris);
+    for (uint32_t i : e.indices) if (i >= n_vertices) return RT_ERR_INVALID;
+    e.uv.assign(uv, uv + 2 * (size_t)n_vertices);
+    if (!world_material(e, m)) return RT_ERR_INVALID;
+    const int id = s->builder.add_world_entity(std::move(e));
+    if (entity_id) *entity_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
+rt_status rt_scene_add_two_spheres_scene(rt_scene* s)
+{
+    if (!s) return RT_ERR_INVALID;
+    s->builder.add_two_spheres_scene();
+    s->built = false;
+    return RT_OK;
+}
+
 rt_status rt_scene_build(rt_scene* s)
 {
     if (!s) return RT_ERR_INVALID;
@@ -284,6 +340,7 @@ void rt_destroy(rt_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_wmats); dfree(c->d_plights);
+    dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -307,6 +364,8 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_ltris, s->flat.ltris)) != RT_OK) return r;
     if ((r = upload(c, c->d_wmats, s->flat.wmats)) != RT_OK) return r;
     if ((r = upload(c, c->d_plights, s->flat.plights)) != RT_OK) return r;
+    if ((r = upload(c, c->d_went, s->flat.went)) != RT_OK) return r;
+    if ((r = upload(c, c->d_wtris, s->flat.wtris)) != RT_OK) return r;
     c->hdr = s->flat.hdr;
     c->has_scene = true;
     return RT_OK;
@@ -337,6 +396,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (!c || !cam || !p) return RT_ERR_INVALID;
     if (!c->has_scene) { c->err = "no scene uploaded"; return RT_ERR_STATE; }
     if (!c->d_accum) { c->err = "no viewport (rt_resize)"; return RT_ERR_STATE; }
+    if (c->hdr.n_went > 0 && !(p->flags & RT_RENDER_WHITTED)) { c->err = "a Whitted world renders with RT_RENDER_WHITTED"; return RT_ERR_INVALID; }
     if (p->first_frame == 0) { c->err = "first_frame is 1-based"; return RT_ERR_INVALID; }
     // a survival probability >= 1 never terminates a path in a closed scene (the reference recurses
     // until its stack overflows); reject it, and NaN
@@ -359,6 +419,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
     P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;
     P.wmats = c->d_wmats; P.plights = c->d_plights; P.n_plights = c->hdr.n_plights;
+    P.went = c->d_went; P.wtris = c->d_wtris; P.n_went = c->hdr.n_went;
+    P.max_bounce_depth = c->hdr.max_bounce_depth; P.intersection_correction = c->hdr.intersection_correction;
     std::memcpy(P.sky, c->hdr.sky, sizeof P.sky);
     std::memcpy(P.cam_pos, cam->position, sizeof P.cam_pos);
     std::memcpy(P.iproj, cam->inv_projection, sizeof P.iproj);
@@ -400,7 +462,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     c->last_flags = p->flags;
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
-        if (whitted) {
+        if (whitted && c->hdr.n_went > 0) {
+            HIPC(c, rt_launch_whitted_world(P, count, c->stream, &grid));
+        } else if (whitted) {
             HIPC(c, rt_launch_whitted(P, count, c->stream, &grid));
         } else {
             HIPC(c, rt_launch_megakernel(P, exact, count, lds, grid, c->block, c->stream));
@@ -500,6 +564,34 @@ rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, in
     return RT_OK;
 }
 
+rt_status rt_world_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, int32_t* ent, int32_t* tri, float* tb)
+{
+    if (!c || (n && (!org || !dir || !ent || !tri || !tb))) return RT_ERR_INVALID;
+    if (!c->has_scene || c->hdr.n_went == 0) { c->err = "no Whitted world uploaded"; return RT_ERR_STATE; }
+    if (n == 0) return RT_OK;
+    if (n > 0x7FFFFFFFull) return RT_ERR_INVALID;
+    HIPC(c, hipSetDevice(c->device));
+    float *d_o = nullptr, *d_d = nullptr, *d_tb = nullptr; int32_t *d_e = nullptr, *d_t = nullptr;
+    auto cleanup = [&]() { dfree(d_o); dfree(d_d); dfree(d_tb); dfree(d_e); dfree(d_t); };
+    KParams P{};
+    P.went = c->d_went; P.wtris = c->d_wtris; P.n_went = c->hdr.n_went;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_o, n * 12)) != hipSuccess || (e = hipMalloc((void**)&d_d, n * 12)) != hipSuccess ||
+        (e = hipMalloc((void**)&d_tb, n * 12)) != hipSuccess || (e = hipMalloc((void**)&d_e, n * 4)) != hipSuccess ||
+        (e = hipMalloc((void**)&d_t, n * 4)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_o, org, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = rt_launch_world_trace(P, (uint32_t)n, d_o, d_d, d_e, d_t, d_tb, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(ent, d_e, n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(tri, d_t, n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(tb, d_tb, n * 12, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_world_trace");
+    }
+    cleanup();
+    return RT_OK;
+}
+
 rt_status rt_math_selftest(rt_ctx* c, uint64_t n, const float* x, float* out)
 {
     if (!c || (n && (!x || !out))) return RT_ERR_INVALID;
@@ -507,12 +599,12 @@ rt_status rt_math_selftest(rt_ctx* c, uint64_t n, const float* x, float* out)
     HIPC(c, hipSetDevice(c->device));
     float *d_x = nullptr, *d_out = nullptr;
     hipError_t e;
-    if ((e = hipMalloc((void**)&d_x, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 24)) != hipSuccess) {
+    if ((e = hipMalloc((void**)&d_x, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 28)) != hipSuccess) {
         dfree(d_x); dfree(d_out); return hip_fail(c, e, "hipMalloc(selftest)");
     }
     if ((e = hipMemcpyAsync(d_x, x, n * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
         (e = rt_launch_math((uint32_t)n, d_x, d_out, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(out, d_out, n * 24, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, d_out, n * 28, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         dfree(d_x); dfree(d_out); return hip_fail(c, e, "rt_math_selftest");
     }

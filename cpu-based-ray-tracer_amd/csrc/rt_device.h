@@ -227,6 +227,16 @@ __device__ __forceinline__ float sin_f(float y)
     return (float)r;
 }
 
+// powf of the specular lobe (WH/Renderer.h:287-292: std::powf -> glibc powf).  Evaluated as
+// exp(y * log(x)) in double and rounded once to float: correctly rounded except within ~1e-15 of a
+// rounding boundary, as glibc's powf (double-precision log2/exp2 core) is; x >= 0 here.
+__device__ __forceinline__ float pow_lobe(float x, float y)
+{
+    if (x == 0.0f) return (y > 0.0f) ? 0.0f : ((y == 0.0f) ? 1.0f : __builtin_inff());
+    if (x == 1.0f || y == 0.0f) return 1.0f;
+    return (float)exp((double)y * log((double)x));
+}
+
 __device__ __forceinline__ uint32_t to_u8(float v)
 {   // (uint8_t)(c * 255.0f), MC/Renderer.cpp:17-20 (v in [0,1] after clamp; NaN -> 0 like x86 cvttss2si)
     const float f = v * 255.0f;

@@ -14,6 +14,8 @@ struct KParams {
     float light_area; float light_emission[3]; int has_light;
     // Whitted shading (rt_whitted.hip): per-material (diffuse color, phong_diffuse), point lights, sky
     const float4* wmats; const float4* plights; uint32_t n_plights; float sky[3];
+    // Whitted world (rt_whitted.hip, config C1): entities + their mesh triangles (rt_layout.h)
+    const float4* went; const float4* wtris; uint32_t n_went; int32_t max_bounce_depth; float intersection_correction;
     // camera: position, inverse projection, inverse view (column-major glm mat4)
     float cam_pos[3]; float iproj[16]; float iview[16];
     // image and sampling
@@ -44,6 +46,10 @@ hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool l
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
+// Whitted Style Ray Tracer world (spheres + textured meshes, reflection/refraction recursion), config C1
+hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
+hipError_t rt_launch_world_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* ent, int32_t* tri, float* tb,
+                                 hipStream_t stream);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);
 

@@ -615,13 +615,14 @@ __global__ void math_kernel(uint32_t n, const float* __restrict__ x, float* __re
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float v = x[i];
-    out[6 * i + 0] = __builtin_sqrtf(v);
-    out[6 * i + 1] = 1.0f / v;
-    out[6 * i + 2] = cos_f(v);
-    out[6 * i + 3] = sin_f(v);
+    out[7 * i + 0] = __builtin_sqrtf(v);
+    out[7 * i + 1] = 1.0f / v;
+    out[7 * i + 2] = cos_f(v);
+    out[7 * i + 3] = sin_f(v);
     const double r = 1.0 / (double)v;
-    out[6 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
-    out[6 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));
+    out[7 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
+    out[7 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));
+    out[7 * i + 6] = pow_lobe(v, 25.0f);   // the C1 specular lobe, powf(x, specular_size_factor = 25)
 }
 
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream)

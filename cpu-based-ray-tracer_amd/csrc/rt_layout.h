@@ -25,6 +25,14 @@
 //            material: (diffuse color, phong_diffuse)
 //  plights : point lights in insertion order (BV/LightSource.h, BV/Renderer.cpp:38-39):
 //            2 x float4 per light: (position, 0), (radiance, 0)
+//  went    : the Whitted Style Ray Tracer's world (config C1, WH/World.h): entities in insertion
+//            order, intersected brute force (WH/Renderer.h:109-140), 4 x float4 per entity:
+//              q0 = (bits(kind: 0 sphere, 1 triangle mesh), bits(material nature), bits(first wtri), bits(n tris))
+//              q1 = (sphere center.xyz, radius)
+//              q2 = (radius^2, refractive_index, phong_diffuse, phong_specular)
+//              q3 = (diffuse_color.xyz, specular_size_factor)          (WH/Entity.h:49-55)
+//  wtris   : triangles of the world's meshes, 4 x float4 per triangle:
+//              (v1.xyz, uv1.x), (v2.xyz, uv1.y), (v3.xyz, uv2.x), (uv2.y, uv3.x, uv3.y, 0)
 #ifndef RT_LAYOUT_H
 #define RT_LAYOUT_H
 #include <stdint.h>
@@ -42,6 +50,14 @@ typedef struct {
     uint32_t max_depth;        // deepest node level (for diagnostics)
     uint32_t n_plights;        // point lights (Whitted shading)
     float sky[3];              // Whitted miss color (BV/Renderer.h:189)
+    uint32_t n_went, n_wtris;  // Whitted world (config C1): entities and mesh triangles
+    int32_t max_bounce_depth;  // WH/World.h:55
+    float intersection_correction;   // WH/World.h:56
 } rt_scene_header;
+
+#define RT_WENT_QUADS 4
+#define RT_WTRI_QUADS 4
+#define RT_WORLD_SPHERE 0
+#define RT_WORLD_MESH 1
 
 #endif

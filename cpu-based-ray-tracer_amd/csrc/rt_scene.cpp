@@ -215,10 +215,82 @@ int SceneBuilder::add_mesh(MeshDesc m)
     return (int)meshes_.size() - 1;
 }
 
+void SceneBuilder::add_two_spheres_scene()
+{
+    // WH/Renderer.cpp:29-48: glm::vec3(-1, 0, -12) r 2 diffuse (0.6, 0.7, 0.8); glass (0.5, -0.5, -8) r 1.5,
+    // refractive index 1.5; the 10x10 chessboard at y = -3 (indices 0 1 3 / 1 2 3, uv corners); two lights
+    WorldEntity diffuse;
+    diffuse.kind = 0; diffuse.center = F3{-1.0f, 0.0f, -12.0f}; diffuse.radius = 2.0f; diffuse.nature = 2;
+    diffuse.diffuse_color = F3{(float)0.6, (float)0.7, (float)0.8};
+    add_world_entity(diffuse);
+    WorldEntity glass;
+    glass.kind = 0; glass.center = F3{(float)0.5, (float)-0.5, -8.0f}; glass.radius = 1.5f; glass.nature = 1;
+    glass.refractive_index = (float)1.5;
+    add_world_entity(glass);
+    WorldEntity board;
+    board.kind = 1; board.nature = 2;
+    board.vertices = {{-5, -3, -6}, {5, -3, -6}, {5, -3, -16}, {-5, -3, -16}};
+    board.indices = {0, 1, 3, 1, 2, 3};
+    board.uv = {0, 0, 1, 0, 1, 1, 0, 1};
+    add_world_entity(board);
+    add_point_light(PointLight{{-20.0f, 70.0f, 20.0f}, {0.5f, 0.5f, 0.5f}});
+    add_point_light(PointLight{{30.0f, 50.0f, -12.0f}, {0.5f, 0.5f, 0.5f}});
+}
+
+// World entities -> went / wtris (rt_layout.h)
+static void flatten_world(const std::vector<WorldEntity>& world, FlatScene& out)
+{
+    uint32_t ntri = 0;
+    for (const auto& e : world) {
+        out.went.resize(out.went.size() + 16);
+        float* q = &out.went[out.went.size() - 16];
+        const uint32_t nt = e.kind == 1 ? (uint32_t)(e.indices.size() / 3) : 0u;
+        q[0] = bits_as_float(e.kind); q[1] = bits_as_float(e.nature); q[2] = bits_as_float((int)ntri); q[3] = bits_as_float((int)nt);
+        q[4] = e.center.x; q[5] = e.center.y; q[6] = e.center.z; q[7] = e.radius;
+        q[8] = e.radius * e.radius;   // Sphere::radius_squared, WH/Sphere.h:19-22
+        q[9] = e.refractive_index; q[10] = e.phong_diffuse; q[11] = e.phong_specular;
+        q[12] = e.diffuse_color.x; q[13] = e.diffuse_color.y; q[14] = e.diffuse_color.z; q[15] = e.specular_size_factor;
+        for (uint32_t t = 0; t < nt; ++t) {
+            const uint32_t i1 = e.indices[3 * t], i2 = e.indices[3 * t + 1], i3 = e.indices[3 * t + 2];
+            const F3 a = e.vertices[i1], b = e.vertices[i2], c = e.vertices[i3];
+            const float w[16] = {a.x, a.y, a.z, e.uv[2 * i1], b.x, b.y, b.z, e.uv[2 * i1 + 1],
+                                 c.x, c.y, c.z, e.uv[2 * i2], e.uv[2 * i2 + 1], e.uv[2 * i3], e.uv[2 * i3 + 1], 0.0f};
+            out.wtris.insert(out.wtris.end(), w, w + 16);
+        }
+        ntri += nt;
+    }
+    out.hdr.n_went = (uint32_t)world.size();
+    out.hdr.n_wtris = ntri;
+}
+
 bool SceneBuilder::build(FlatScene& out, std::string& err) const
 {
     out = FlatScene{};
     const size_t nm = meshes_.size();
+    for (const auto& e : world_) {
+        if (e.kind == 0 && !(e.radius > 0.0f)) { err = "world sphere with a non-positive radius"; return false; }
+        if (e.kind == 1) {
+            if (e.indices.empty() || e.indices.size() % 3 || e.uv.size() != 2 * e.vertices.size()) { err = "bad world mesh"; return false; }
+            for (uint32_t i : e.indices) if (i >= e.vertices.size()) { err = "world mesh index out of range"; return false; }
+        }
+    }
+    if (nm == 0 && !world_.empty()) {
+        // a pure Whitted world (config C1): no BVH, brute-force entities
+        flatten_world(world_, out);
+        out.plights.resize(lights_.size() * 8);
+        for (size_t k = 0; k < lights_.size(); ++k) {
+            float* q = &out.plights[8 * k];
+            q[0] = lights_[k].position.x; q[1] = lights_[k].position.y; q[2] = lights_[k].position.z; q[3] = 0.0f;
+            q[4] = lights_[k].radiance.x; q[5] = lights_[k].radiance.y; q[6] = lights_[k].radiance.z; q[7] = 0.0f;
+        }
+        out.hdr.n_plights = (uint32_t)lights_.size();
+        out.hdr.sky[0] = sky_.x; out.hdr.sky[1] = sky_.y; out.hdr.sky[2] = sky_.z;
+        out.hdr.light_mesh = -1;
+        out.hdr.max_bounce_depth = 5;               // WH/World.h:55
+        out.hdr.intersection_correction = 0.00001f; // WH/World.h:56
+        return true;
+    }
+    if (!world_.empty()) { err = "a scene holds either triangle meshes or a Whitted world, not both"; return false; }
     if (nm == 0) { err = "empty scene"; return false; }
     // ---- per mesh: triangles, mesh box, total area, mesh BVH (TriangleMesh ctor)
     std::vector<std::vector<Tri>> tris(nm);

@@ -28,10 +28,25 @@ struct MeshDesc {
 
 struct PointLight { F3 position; F3 radiance; };
 
+// An entity of the Whitted Style Ray Tracer's world (WH/Entity.h:16-57, WH/Sphere.h, WH/TriangleMesh.h).
+// nature: 0 Reflective, 1 Reflective_Refractive, 2 Diffuse_Glossy (WH/WhittedUtilities.h:18-23).
+struct WorldEntity {
+    int kind = 0;                       // 0 sphere, 1 indexed triangle mesh
+    F3 center{0, 0, 0};
+    float radius = 0.0f;
+    std::vector<F3> vertices;           // mesh: vertex positions
+    std::vector<uint32_t> indices;      // mesh: 3 per triangle
+    std::vector<float> uv;              // mesh: 2 per vertex
+    int nature = 2;
+    float refractive_index = 1.3f, phong_diffuse = 0.8f, phong_specular = 0.2f, specular_size_factor = 25.0f;
+    F3 diffuse_color{0.2f, 0.2f, 0.2f};
+};
+
 // Flattened, upload-ready scene (rt_layout.h).
 struct FlatScene {
     rt_scene_header hdr{};
     std::vector<float> nodes, tris, mats, lnodes, ltris, wmats, plights;   // float4-granular
+    std::vector<float> went, wtris;                                       // Whitted world (C1)
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag
     std::vector<float> dbg_node_f;    // 7 per node
     std::vector<int32_t> dbg_node_i;  // 5 per node
@@ -51,6 +66,10 @@ public:
     // Renderer::Add(std::unique_ptr<PointLightSource>), BV/Renderer.h:88-97
     void add_point_light(const PointLight& l) { lights_.push_back(l); }
     void set_sky(const F3& c) { sky_ = c; }
+    // World::Add(std::unique_ptr<Entity>) (WH/World.h:37-45)
+    int add_world_entity(WorldEntity e) { world_.push_back(std::move(e)); return (int)world_.size() - 1; }
+    // the world of the Whitted Style Ray Tracer's Renderer::Renderer() (WH/Renderer.cpp:27-49)
+    void add_two_spheres_scene();
     // Renderer::GenerateBVH (MC/Renderer.h:83-86) + TriangleMesh's per-mesh BVH (MC/TriangleMesh.h:185)
     bool build(FlatScene& out, std::string& err) const;
     size_t num_meshes() const { return meshes_.size(); }
@@ -59,6 +78,7 @@ public:
 private:
     std::vector<MeshDesc> meshes_;
     std::vector<PointLight> lights_;
+    std::vector<WorldEntity> world_;
     F3 sky_{0.2f, 0.7f, 0.8f};   // BV/Renderer.h:189
 };
 

@@ -19,6 +19,7 @@
 
 #include "rt_device.h"
 #include "rt_kernels.h"
+#include "rt_layout.h"
 
 using namespace rtd;
 
@@ -154,5 +155,322 @@ hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, u
     if (tiles == 0) return hipSuccess;
     if (count) hipLaunchKernelGGL(whitted_kernel<true>, dim3(tiles), dim3(256), 0, stream, P);
     else hipLaunchKernelGGL(whitted_kernel<false>, dim3(tiles), dim3(256), 0, stream, P);
+    return hipGetLastError();
+}
+
+// =============================================================================================
+// The Whitted Style Ray Tracer's world (config C1; WH/ = "Whitted Style Ray Tracer/8599RayTracerGUI/src/"):
+// spheres and textured triangle meshes intersected brute force in insertion order
+// (get_intersection_payload, WH/Renderer.h:109-140), shaded by cast_Whitted_ray (WH/Renderer.h:184-310):
+// Diffuse_Glossy ends the ray with two shadowed point lights (diffuse + Phong specular), Reflective and
+// Reflective_Refractive recurse with Fresnel weights to depth 5.  The recursion is a per-lane explicit
+// stack evaluated in the reference's post-order (reflected child, then refracted child, then the
+// weighted sum), so every float operation happens in the reference's order.  One thread per pixel.
+// =============================================================================================
+namespace {
+
+struct WHit { int ent; int tri; float t; float b2, b3; };
+
+// QuadraticFormula, WH/WhittedUtilities.h:38-60 (the -0.5 literals are double)
+__device__ __forceinline__ bool quadratic(float A, float B, float C, float& xs, float& xl)
+{
+    const float disc = B * B - 4.0f * A * C;
+    if (disc < 0.0f) return false;
+    if (disc == 0.0f) {
+        xs = xl = (float)((-0.5 * (double)B) / (double)A);
+    } else {
+        const float sq = __builtin_sqrtf(disc);
+        const float q = (float)((B > 0.0f) ? (-0.5 * (double)(B + sq)) : (-0.5 * (double)(B - sq)));
+        xs = q / A;
+        xl = C / q;
+    }
+    if (xs > xl) { const float t = xs; xs = xl; xl = t; }
+    return true;
+}
+
+// Sphere::Intersect, WH/Sphere.h:26-59
+__device__ __forceinline__ bool sphere_hit(const float4& c, float r2, const V3& o, const V3& d, float& t)
+{
+    const V3 oc = sub(o, V3{c.x, c.y, c.z});
+    float ts, tl;
+    if (!quadratic(dot(d, d), 2.0f * dot(d, oc), dot(oc, oc) - r2, ts, tl)) return false;
+    if (ts < 0.0f) ts = tl;
+    if (ts < 0.0f) return false;
+    t = ts;
+    return true;
+}
+
+// Whitted::RayTriangleIntersection (all float), WH/TriangleMesh.h:16-45
+__device__ __forceinline__ bool tri_hit_f32(const V3& v1, const V3& v2, const V3& v3, const V3& o, const V3& d, float& t, float& b2, float& b3)
+{
+    const V3 E1 = sub(v2, v1), E2 = sub(v3, v1), S = sub(o, v1);
+    const V3 S1 = cross(d, E2), S2 = cross(S, E1);
+    const float den = dot(S1, E1);
+    t = dot(S2, E2) / den;
+    b2 = dot(S1, S) / den;
+    b3 = dot(S2, d) / den;
+    return (t > 0.0f) && (b2 > 0.0f) && (b3 > 0.0f) && (((1.0f - b2) - b3) > 0.0f);
+}
+
+// get_intersection_payload, WH/Renderer.h:109-140: entities in order, strict '<' (the first of equal
+// t wins; inside a mesh, TriangleMesh::Intersect, WH/TriangleMesh.h:86-112, likewise)
+__device__ __forceinline__ bool world_hit(const KParams& P, const V3& o, const V3& d, WHit& h)
+{
+    const float FMAX = 3.40282347e+38f;   // Whitted::positive_infinity
+    float t_closest = FMAX;
+    bool any = false;
+    for (uint32_t e = 0; e < P.n_went; ++e) {
+        const float4 q0 = P.went[4 * e], q1 = P.went[4 * e + 1], q2 = P.went[4 * e + 2];
+        float t_local = FMAX;
+        int tri = -1;
+        float b2 = 0.0f, b3 = 0.0f;
+        bool hit = false;
+        if (f2i(q0.x) == RT_WORLD_SPHERE) {
+            hit = sphere_hit(q1, q2.x, o, d, t_local);
+        } else {
+            const int first = f2i(q0.z), nt = f2i(q0.w);
+            for (int k = 0; k < nt; ++k) {
+                const float4 a = P.wtris[4 * (first + k)], b = P.wtris[4 * (first + k) + 1], c = P.wtris[4 * (first + k) + 2];
+                float t, u, v;
+                if (tri_hit_f32(V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, V3{c.x, c.y, c.z}, o, d, t, u, v) && t < t_local) {
+                    t_local = t; b2 = u; b3 = v; tri = first + k; hit = true;
+                }
+            }
+        }
+        if (hit && t_local < t_closest) {
+            t_closest = t_local;
+            h = WHit{(int)e, tri, t_local, b2, b3};
+            any = true;
+        }
+    }
+    return any;
+}
+
+// mirror_reflection_direction, WH/Renderer.h:41-45
+__device__ __forceinline__ V3 mirror_dir(const V3& I, const V3& N) { return sub(I, smul(2.0f * dot(I, N), N)); }
+
+__device__ __forceinline__ float clamp_float(float v, float lo, float hi) { return smax(smin(v, hi), lo); }   // WH/WhittedUtilities.h:33-36
+
+// snell_refraction_direction, WH/Renderer.h:47-76
+__device__ __forceinline__ V3 snell_dir(const V3& I, const V3& N, float eta)
+{
+    float eta_in = 1.0f, eta_out = eta;
+    V3 normal = N;
+    float ci = clamp_float(dot(I, N), -1.0f, 1.0f);
+    if (ci < 0.0f) ci = -ci;
+    else { const float t = eta_in; eta_in = eta_out; eta_out = t; normal = neg(normal); }
+    const float er = eta_in / eta_out;
+    const float k = 1.0f - er * er * (1.0f - ci * ci);
+    return (k < 0.0f) ? V3{0.0f, 0.0f, 0.0f} : add(smul(er, I), smul(er * ci - __builtin_sqrtf(k), normal));
+}
+
+// accurate_fresnel_reflectance, WH/Renderer.h:78-107
+__device__ __forceinline__ float fresnel(const V3& I, const V3& N, float eta)
+{
+    float eta_in = 1.0f, eta_out = eta;
+    float ci = clamp_float(dot(I, N), -1.0f, 1.0f);
+    if (ci < 0.0f) ci = -ci;
+    else { const float t = eta_in; eta_in = eta_out; eta_out = t; }
+    const float st = eta_in / eta_out * __builtin_sqrtf(smax(0.0f, 1.0f - ci * ci));
+    if (st > 1.0f) return 1.0f;
+    const float ct = __builtin_sqrtf(smax(0.0f, 1.0f - st * st));
+    const float rs = (eta_in * ci - eta_out * ct) / (eta_in * ci + eta_out * ct);
+    const float rp = (eta_in * ct - eta_out * ci) / (eta_in * ct + eta_out * ci);
+    return (rs * rs + rp * rp) / 2.0f;
+}
+
+// TriangleMesh::GetDiffuseColor (the chessboard texture), WH/TriangleMesh.h:79-84; fmodf(v, 1) of a
+// finite v is v - trunc(v), exactly
+__device__ __forceinline__ V3 checker(float u, float v)
+{
+    const float a = u * 5.0f, b = v * 5.0f;
+    const float fa = a - __builtin_truncf(a), fb = b - __builtin_truncf(b);
+    const float pattern = ((fa > 0.5f) != (fb > 0.5f)) ? 1.0f : 0.0f;
+    const V3 c0{(float)0.815, (float)0.235, (float)0.031}, c1{(float)0.937, (float)0.937, (float)0.231};
+    return add(muls(c0, 1.0f - pattern), muls(c1, pattern));   // Whitted::lerp, WH/VectorFloat.h:16-19
+}
+
+struct WFrame {
+    V3 o, d;
+    int depth, stage;   // stage 0: trace; 1: reflected child done; 2: refracted child done; 3: mirror child done
+    float R;
+    V3 acc, to, td;
+};
+constexpr int kWorldFrames = 8;
+
+template <bool COUNT>
+__device__ V3 cast_whitted_world(const KParams& P, const V3& o0, const V3& d0, uint32_t& rays)
+{
+    WFrame st[kWorldFrames];
+    int sp = 0;
+    st[0].o = o0; st[0].d = d0; st[0].depth = 0; st[0].stage = 0;
+    sp = 1;
+    V3 ret{0.0f, 0.0f, 0.0f};
+    const float eps = P.intersection_correction;
+    while (sp > 0) {
+        WFrame& F = st[sp - 1];
+        if (F.stage == 0) {
+            if (F.depth > P.max_bounce_depth || (F.d.x == 0.0f && F.d.y == 0.0f && F.d.z == 0.0f)) {
+                ret = V3{0.0f, 0.0f, 0.0f};   // no energy received
+                --sp;
+                continue;
+            }
+            if (COUNT) ++rays;
+            WHit h;
+            if (!world_hit(P, F.o, F.d, h)) {
+                ret = V3{P.sky[0], P.sky[1], P.sky[2]};
+                --sp;
+                continue;
+            }
+            const float4 e0 = P.went[4 * h.ent], e1 = P.went[4 * h.ent + 1], e2 = P.went[4 * h.ent + 2], e3 = P.went[4 * h.ent + 3];
+            const V3 x = add(F.o, muls(F.d, h.t));
+            V3 n;
+            float tu = 0.0f, tv = 0.0f;
+            if (f2i(e0.x) == RT_WORLD_SPHERE) {
+                n = w_normalize(sub(x, V3{e1.x, e1.y, e1.z}));   // Sphere::GetHitInfo, WH/Sphere.h:61-72
+            } else {
+                // TriangleMesh::GetHitInfo, WH/TriangleMesh.h:114-136
+                const float4 a = P.wtris[4 * h.tri], b = P.wtris[4 * h.tri + 1], c = P.wtris[4 * h.tri + 2], u = P.wtris[4 * h.tri + 3];
+                const V3 v1{a.x, a.y, a.z}, v2{b.x, b.y, b.z}, v3{c.x, c.y, c.z};
+                n = w_normalize(cross(w_normalize(sub(v2, v1)), w_normalize(sub(v3, v2))));
+                const float s = (1.0f - h.b2) - h.b3;
+                tu = (s * a.w + h.b2 * c.w) + h.b3 * u.y;
+                tv = (s * b.w + h.b2 * u.x) + h.b3 * u.z;
+            }
+            const int nature = f2i(e0.y);
+            const float eta = e2.y;
+            if (nature == 0 || nature == 1) {
+                const V3 rd = w_normalize(mirror_dir(F.d, n));
+                const V3 ro = (dot(rd, n) < 0.0f) ? sub(x, muls(n, eps)) : add(x, muls(n, eps));
+                if (nature == 0) {
+                    F.R = fresnel(neg(rd), n, eta);
+                    F.stage = 3;
+                } else {
+                    F.td = w_normalize(snell_dir(F.d, n, eta));
+                    F.to = (dot(F.td, n) < 0.0f) ? sub(x, muls(n, eps)) : add(x, muls(n, eps));
+                    F.R = fresnel(F.d, n, eta);
+                    F.stage = 1;
+                }
+                WFrame& C = st[sp];
+                C.o = ro; C.d = rd; C.depth = F.depth + 1; C.stage = 0;
+                ++sp;
+                continue;
+            }
+            // Diffuse_Glossy (WH/Renderer.h:261-305)
+            V3 diff{0.0f, 0.0f, 0.0f}, spec{0.0f, 0.0f, 0.0f};
+            const V3 spt = (dot(F.d, n) < 0.0f) ? add(x, muls(n, eps)) : sub(x, muls(n, eps));
+            for (uint32_t l = 0; l < P.n_plights; ++l) {
+                const float4 lp = P.plights[2 * l], lr4 = P.plights[2 * l + 1];
+                V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
+                const float d2 = dot(ld, ld);
+                ld = w_normalize(ld);
+                if (COUNT) ++rays;
+                WHit oh;
+                if (world_hit(P, spt, ld, oh) && (oh.t * oh.t < d2)) continue;
+                const V3 rad{lr4.x, lr4.y, lr4.z};
+                diff = add(diff, muls(rad, __builtin_fabsf(dot(ld, n))));
+                const float lobe = pow_lobe(smax(0.0f, -dot(mirror_dir(neg(ld), n), F.d)), e3.w);
+                spec = add(spec, smul(lobe, rad));
+            }
+            const V3 dc = (f2i(e0.x) == RT_WORLD_SPHERE) ? V3{e3.x, e3.y, e3.z} : checker(tu, tv);
+            ret = add(muls(mul(diff, dc), e2.z), muls(spec, e2.w));
+            --sp;
+        } else if (F.stage == 1) {
+            // the reflected color is in; trace the refracted ray
+            F.acc = ret;
+            F.stage = 2;
+            WFrame& C = st[sp];
+            C.o = F.to; C.d = F.td; C.depth = F.depth + 1; C.stage = 0;
+            ++sp;
+        } else if (F.stage == 2) {
+            ret = add(smul(F.R, F.acc), smul(1.0f - F.R, ret));   // reflectance * reflected + (1 - reflectance) * refracted
+            --sp;
+        } else {
+            ret = muls(ret, F.R);   // cast_Whitted_ray(reflected) * fresnel
+            --sp;
+        }
+    }
+    return ret;
+}
+
+}  // namespace
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256) whitted_world_kernel(KParams P)
+{
+    const uint32_t tiles_x = (P.W + 15) / 16;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t lr = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
+    const uint32_t lx = (tile % tiles_x) * 16 + (threadIdx.x & 15);
+    uint32_t rays = 0;
+    if (lr < P.n_local_rows && lx < P.W) {
+        const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
+        const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
+        const uint32_t local = lr * P.W + lx;
+        float4 acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
+        float cam_x = P.cam_pos[0];
+        for (uint32_t k = 0; k < P.n_frames; ++k) {
+            asm volatile("" : "+v"(cam_x));   // every frame is evaluated, as the reference does
+            // Camera::RecomputeRayDirections, WH/Camera.cpp:114-132: bottom-left corner of the pixel
+            float cx = (float)lx / (float)P.W;
+            float cy = (float)y / (float)P.H;
+            cx = cx * 2.0f - 1.0f;
+            cy = cy * 2.0f - 1.0f;
+            float tg[4];
+            mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
+            const V3 dv = glm_normalize(divs(V3{tg[0], tg[1], tg[2]}, tg[3]));
+            float wd[4];
+            mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
+            const V3 cam{cam_x, P.cam_pos[1], P.cam_pos[2]};
+            // RayGen_Shader, WH/Renderer.cpp:116-125
+            const V3 color = cast_whitted_world<COUNT>(P, cam, w_normalize(V3{wd[0], wd[1], wd[2]}), rays);
+            acc.x = acc.x + color.x; acc.y = acc.y + color.y; acc.z = acc.z + color.z; acc.w = acc.w + 1.0f;
+        }
+        if (P.n_frames > 0) {
+            const float fr = (float)(P.first_frame + P.n_frames - 1u);
+            const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
+            const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
+            P.accum[local] = acc;
+            P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+        }
+    }
+    if (COUNT) {
+        uint64_t c = rays;
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off);
+        if (__lane_id() == 0) atomicAdd((unsigned long long*)&P.counters[2], (unsigned long long)c);
+    }
+}
+
+hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out)
+{
+    const uint32_t tiles = ((P.W + 15) / 16) * ((P.n_local_rows + 15) / 16);
+    if (grid_out) *grid_out = tiles;
+    if (tiles == 0) return hipSuccess;
+    if (P.max_bounce_depth + 2 > kWorldFrames) return hipErrorInvalidValue;   // the explicit stack bounds the recursion
+    if (count) hipLaunchKernelGGL(whitted_world_kernel<true>, dim3(tiles), dim3(256), 0, stream, P);
+    else hipLaunchKernelGGL(whitted_world_kernel<false>, dim3(tiles), dim3(256), 0, stream, P);
+    return hipGetLastError();
+}
+
+// closest hit of n rays against the world (unit-test entry point: rt_world_trace)
+__global__ void __launch_bounds__(256) world_trace_kernel(KParams P, uint32_t n, const float* __restrict__ org, const float* __restrict__ dir,
+                                                          int32_t* __restrict__ ent, int32_t* __restrict__ tri, float* __restrict__ tb)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    WHit h;
+    const bool hit = world_hit(P, V3{org[3 * i], org[3 * i + 1], org[3 * i + 2]}, V3{dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]}, h);
+    ent[i] = hit ? h.ent : -1;
+    tri[i] = hit ? h.tri : -1;
+    tb[3 * i] = hit ? h.t : 0.0f;
+    tb[3 * i + 1] = hit && h.tri >= 0 ? h.b2 : 0.0f;
+    tb[3 * i + 2] = hit && h.tri >= 0 ? h.b3 : 0.0f;
+}
+
+hipError_t rt_launch_world_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* ent, int32_t* tri, float* tb,
+                                 hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(world_trace_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, P, n, org, dir, ent, tri, tb);
     return hipGetLastError();
 }

@@ -18,6 +18,11 @@
  *   rt_trace                              Renderer::ray_BVH_intersection_record             MC/Renderer.h:88-91
  *   rt_render + RT_RENDER_WHITTED         BVH Ray Tracer Renderer::Render / cast_Whitted_ray   BV/Renderer.cpp:69-233
  *   rt_scene_add_bvh_tracer_scene         BVH Ray Tracer Renderer::Renderer()                  BV/Renderer.cpp:26-43
+ *   rt_scene_add_world_sphere / _mesh     Whitted Style Ray Tracer Sphere / TriangleMesh + World::Add
+ *                                         (WH/Sphere.h:16-75, WH/TriangleMesh.h:47-155, WH/World.h:37-45)
+ *   rt_scene_add_two_spheres_scene        Whitted Style Ray Tracer Renderer::Renderer()       WH/Renderer.cpp:27-49
+ *   rt_render + RT_RENDER_WHITTED on a    Whitted Style Ray Tracer RayGen_Shader /           WH/Renderer.cpp:82-125,
+ *     world scene                         cast_Whitted_ray                                   WH/Renderer.h:184-310
  */
 #ifndef RT_CAPI_H
 #define RT_CAPI_H
@@ -64,6 +69,30 @@ rt_status rt_scene_add_point_light(rt_scene* s, const float position[3], const f
 rt_status rt_scene_set_sky(rt_scene* s, const float rgb[3]);
 /* the BVH Ray Tracer's Renderer::Renderer() scene (BV/Renderer.cpp:26-43) from the two OBJ files */
 rt_status rt_scene_add_bvh_tracer_scene(rt_scene* s, const char* bunny_obj, const char* teapot_obj);
+
+/* The Whitted Style Ray Tracer's world (WH/ = Whitted Style Ray Tracer/8599RayTracerGUI/src/): entities
+ * intersected brute force in insertion order, Whitted recursion to depth 5 with Fresnel reflection /
+ * Snell refraction (WH/Renderer.h:184-310).  A scene holds either such a world or triangle meshes. */
+#define RT_REFLECTIVE 0
+#define RT_REFLECTIVE_REFRACTIVE 1
+#define RT_DIFFUSE_GLOSSY 2
+typedef struct {
+    int32_t nature;               /* RT_REFLECTIVE / RT_REFLECTIVE_REFRACTIVE / RT_DIFFUSE_GLOSSY */
+    float refractive_index;       /* WH/Entity.h defaults: 1.3 */
+    float phong_diffuse;          /* 0.8 */
+    float phong_specular;         /* 0.2 */
+    float specular_size_factor;   /* 25 */
+    float diffuse_color[3];       /* (0.2, 0.2, 0.2); triangle meshes use the chessboard texture instead
+                                     (TriangleMesh::GetDiffuseColor, WH/TriangleMesh.h:79-84) */
+} rt_world_material;
+/* fills *m with the WH/Entity.h defaults */
+void rt_world_material_default(rt_world_material* m);
+rt_status rt_scene_add_world_sphere(rt_scene* s, const float center[3], float radius, const rt_world_material* m, int32_t* entity_id);
+/* indexed mesh: n_vertices positions (3 floats) + texture coordinates (2 floats), 3 indices per triangle */
+rt_status rt_scene_add_world_mesh(rt_scene* s, const float* vertices, uint32_t n_vertices, const uint32_t* indices, uint32_t n_tris,
+                                  const float* uv, const rt_world_material* m, int32_t* entity_id);
+/* Renderer::Renderer() of the Whitted Style Ray Tracer: diffuse + glass sphere, chessboard, two lights */
+rt_status rt_scene_add_two_spheres_scene(rt_scene* s);
 rt_status rt_scene_build(rt_scene* s);
 
 typedef struct {
@@ -150,8 +179,11 @@ rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 
 /* closest hit of n rays (host arrays; tri = flattened triangle slot or -1, t = double distance) */
 rt_status rt_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t);
+/* closest hit of n rays against a Whitted world (get_intersection_payload, WH/Renderer.h:109-140):
+ * entity index or -1, mesh triangle slot or -1, and (t, barycentric 2, barycentric 3) as 3 floats */
+rt_status rt_world_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* entity, int32_t* tri, float* t_bary);
 /* device arithmetic self-test: for each x: sqrtf, 1/x, cos, sin (as the kernel evaluates them),
- * and the double reciprocal's low/high words -> 6 floats per input */
+ * the double reciprocal's low/high words, and the C1 specular lobe powf(x, 25) -> 7 floats per input */
 rt_status rt_math_selftest(rt_ctx* ctx, uint64_t n, const float* x, float* out);
 
 int32_t rt_api_version(void);

@@ -8,6 +8,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
 
     python oracle/gen_golden.py            # all fixtures
     python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
+    python oracle/gen_golden.py c1         # only the C1 (Whitted two-sphere world) fixtures
     python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
 """
@@ -419,9 +420,78 @@ def gen_c5(rng):
     np.savez_compressed(os.path.join(GOLDEN, "c5_scene.npz"), **out)
 
 
+# ------------------------------------------------------------------ Whitted Style Ray Tracer (config C1)
+HARNESS_WH = os.path.join(HERE, "_ref", "ref_whitted_spheres")
+WH_HIT_DT = np.dtype([("ent", "<i4"), ("tri", "<i4"), ("t", "<f4"), ("b2", "<f4"), ("b3", "<f4")])
+
+
+def run_wh(*args):
+    r = subprocess.run([HARNESS_WH] + [str(a) for a in args], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"ref_whitted_spheres {args[0]} failed: {r.returncode} {r.stderr}")
+    print(" ", r.stdout.strip())
+
+
+def gen_c1(rng):
+    """C1: the two-sphere Whitted world through the reference's own Sphere / TriangleMesh / Camera code
+    (shading recursion restated, see oracle/ref/ref_whitted_spheres.cpp)."""
+    import hashlib
+    out = {}
+    for (W, H) in [(16, 12), (640, 480), (160, 120)]:
+        run_wh("camera", W, H, tmp("wh_cam"))
+        b = np.fromfile(tmp("wh_cam"), np.uint8)
+        out[f"mats_{W}x{H}"] = b[:256].view("<f4").reshape(4, 4, 4)
+        out[f"vec_{W}x{H}"] = b[256:280].view("<f4")
+        if W * H <= 4096:
+            out[f"dirs_{W}x{H}"] = b[280:].view("<f4").reshape(-1, 3)
+    # closest hits: camera rays at the objects, random rays (incl. from inside the glass sphere),
+    # rays at the chessboard's vertices and shared diagonal (ties between its two triangles)
+    n = 4096
+    cam = np.array([0, 0, 6], np.float32)
+    o, d = [], []
+    k = 1500
+    tgt = rng.uniform([-6, -3.5, -17], [6, 3, -5], (k, 3)).astype(np.float32)
+    o.append(np.repeat(cam[None], k, 0)); d.append(tgt - cam)
+    k = 1000
+    o.append(rng.uniform([-6, -2.9, -17], [6, 4, -4], (k, 3)).astype(np.float32)); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    k = 600   # from inside the glass sphere (center (0.5, -0.5, -8), r 1.5)
+    dirv = rng.normal(size=(k, 3)); dirv /= np.linalg.norm(dirv, axis=1, keepdims=True)
+    o.append((np.array([0.5, -0.5, -8]) + dirv * rng.uniform(0, 1.4, (k, 1))).astype(np.float32))
+    d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    k = n - 3100
+    board = np.array([[-5, -3, -6], [5, -3, -6], [5, -3, -16], [-5, -3, -16]], np.float32)
+    w = rng.random(k)
+    a, b = board[1], board[3]   # the shared edge of triangles (0,1,3) and (1,2,3)
+    tgt = np.where((rng.random(k) < 0.5)[:, None], (a[None] * w[:, None] + b[None] * (1 - w[:, None])), board[rng.integers(0, 4, k)])
+    o.append(np.repeat(cam[None], k, 0)); d.append((tgt - cam).astype(np.float32))
+    o = np.concatenate(o).astype(np.float32)
+    d = np.concatenate(d).astype(np.float32)
+    np.concatenate([o, d], 1).astype("<f4").tofile(tmp("wh_rays.in"))
+    run_wh("rays", tmp("wh_rays.in"), tmp("wh_rays.out"))
+    res = np.fromfile(tmp("wh_rays.out"), WH_HIT_DT)
+    out.update(ray_org=o, ray_dir=d, ray_ent=res["ent"], ray_tri=res["tri"], ray_t=res["t"], ray_b2=res["b2"], ray_b3=res["b3"])
+    # glibc powf on specular-lobe arguments (x in [0, 1], exponent 25)
+    x = np.concatenate([rng.random(20000), rng.random(2000) ** 0.01, [0.0, 1.0, 0.5]]).astype(np.float32)
+    pin = np.stack([x, np.full_like(x, 25.0)], 1).astype("<f4")
+    pin.tofile(tmp("pow.in"))
+    run_wh("pow", tmp("pow.in"), tmp("pow.out"))
+    out.update(pow_x=x, pow_y=np.float32(25.0), pow_out=np.fromfile(tmp("pow.out"), "<f4"))
+    for (W, H, spp) in [(640, 480, 1), (160, 120, 3), (97, 61, 2)]:
+        run_wh("image", W, H, spp, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        key = f"{W}x{H}_spp{spp}"
+        out[f"accum_{key}"] = acc
+        out[f"rgba_{key}"] = rgba
+        out[f"sha_accum_{key}"] = np.array(hashlib.sha256(acc.tobytes()).hexdigest())
+        out[f"sha_rgba_{key}"] = np.array(hashlib.sha256(rgba.tobytes()).hexdigest())
+        out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
+    np.savez_compressed(os.path.join(GOLDEN, "c1_spheres.npz"), **out)
+
+
 def main():
     global TMP
-    if not os.path.exists(HARNESS) or not os.path.exists(HARNESS_BV):
+    if not os.path.exists(HARNESS) or not os.path.exists(HARNESS_BV) or not os.path.exists(HARNESS_WH):
         subprocess.check_call(["make", "-C", HERE, "ref"])
     os.makedirs(GOLDEN, exist_ok=True)
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -443,6 +513,8 @@ def main():
             nodes, tris = gen_bvh_scene()
             gen_bvh_rays(nodes, tris, rng)
             gen_bvh_images()
+        if only in ("all", "c1"):
+            gen_c1(np.random.default_rng(20261017))
         if only in ("all", "c5"):
             gen_c5(np.random.default_rng(20261016))
     print("golden fixtures written to", GOLDEN)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-configuration throughput on ONE MI355X (SURVEY.md section 8(d) configs C2, C3, C4, C5).
+"""Per-configuration throughput on ONE MI355X (SURVEY.md section 8(d) configs C1, C2, C3, C4, C5).
 
 bench.py reports the headline (C4); this prints one JSON line per configuration with the megakernel
 time (HIP events on its stream), Msamples/s, and the algorithmic-bytes roofline of SURVEY.md 8(d)
@@ -22,10 +22,12 @@ from _rt import rt  # noqa: E402
 
 HBM_PEAK = 8000.0
 # reference work per sample, SURVEY.md 8(d): rays/sample, node tests/ray, triangle tests/ray
-WORK = {"C2": (5.700, 27.84, 4.06), "C3": (1.446, 38.26, 2.57), "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
+WORK = {"C1": None, "C2": (5.700, 27.84, 4.06), "C3": (1.446, 38.26, 2.57), "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
 
 
 def bytes_per_sample(c):
+    if WORK[c] is None:   # C1: three entities, no BVH; brute force over 2 spheres + 2 triangles
+        return None
     r, n, t = WORK[c]
     return r * (n * 32 + t * 36 + 16)
 
@@ -42,7 +44,7 @@ def run(ctx, cam, W, H, spp, reps, **kw):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="C2,C3,C4,C5")
+    ap.add_argument("--configs", default="C1,C2,C3,C4,C5")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--c5-spp", type=int, default=64)
     ap.add_argument("--fast", action="store_true")
@@ -51,7 +53,12 @@ def main():
     for c in args.configs.split(","):
         ctx = rt.Context(0)
         kw = {}
-        if c in ("C2", "C4"):
+        if c == "C1":
+            ctx.upload(rt.Scene.two_spheres())
+            W, H, spp = 640, 480, 1
+            cam = rt.camera_two_spheres(W, H)
+            kw = dict(whitted=True)
+        elif c in ("C2", "C4"):
             ctx.upload(rt.Scene.cornell())
             W, H, spp = (784, 784, 256) if c == "C2" else (1920, 1080, 1024)
             cam, _, _ = rt.camera_default(W, H)
@@ -73,11 +80,11 @@ def main():
         samples = W * H * spp
         rate = samples / (ms / 1e3)
         bps = bytes_per_sample(c)
+        roof = None if bps is None else {"bytes_per_sample": round(bps, 1), "achieved_gbs": round(bps * rate / 1e9, 1),
+                                         "peak_gbs": HBM_PEAK, "frac": round(bps * rate / 1e9 / HBM_PEAK, 4)}
         print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
-                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid,
-                          "roofline": {"bytes_per_sample": round(bps, 1), "achieved_gbs": round(bps * rate / 1e9, 1),
-                                       "peak_gbs": HBM_PEAK, "frac": round(bps * rate / 1e9 / HBM_PEAK, 4)},
-                          "mode": "whitted" if c == "C3" else ("fast" if args.fast else "exact")}), flush=True)
+                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "roofline": roof,
+                          "mode": "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")}), flush=True)
         ctx.close()
 
 
