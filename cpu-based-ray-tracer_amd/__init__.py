@@ -48,7 +48,14 @@ class Stats(C.Structure):
                 ("stack_depth", C.c_uint32), ("wave_rounds", C.c_uint64), ("wave_steps", C.c_uint64),
                 ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64), ("wave_fold", C.c_uint64),
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
-                ("service_lanes", C.c_uint64)]
+                ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float)]
+
+
+class DenoiseParams(C.Structure):
+    """rt_denoise_params: the Denoiser project's filter settings (DN/Denoiser.h:333-358, DN/Renderer.cpp:108-241)."""
+    _fields_ = [("jbf_half_size", C.c_int32), ("temporal_half_size", C.c_int32), ("tolerance", C.c_float),
+                ("current_frame_weighting", C.c_float), ("immediate_clamp", C.c_int32), ("sigma_position", C.c_float),
+                ("sigma_color", C.c_float), ("sigma_normal", C.c_float), ("sigma_coplanarity", C.c_float)]
 
 
 class WorldMaterial(C.Structure):
@@ -114,6 +121,11 @@ def lib():
         "rt_scene_add_world_mesh": (i32, [vp, fp, u32, C.POINTER(u32), u32, fp, C.POINTER(WorldMaterial), C.POINTER(i32)]),
         "rt_scene_add_two_spheres_scene": (i32, [vp]),
         "rt_world_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(i32), fp]),
+        "rt_camera_look_ex": (i32, [u32, u32, fp, fp, C.c_float, C.c_float, C.c_float, C.POINTER(Camera), fp, fp]),
+        "rt_denoise_params_default": (None, [C.POINTER(DenoiseParams)]),
+        "rt_render_denoised": (i32, [vp, C.POINTER(Camera), fp, fp, u32, u64, C.c_float, C.POINTER(DenoiseParams), C.POINTER(u32), fp]),
+        "rt_denoise_restart": (i32, [vp]),
+        "rt_get_gbuffer": (i32, [vp, fp, fp, fp, C.POINTER(i32), fp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -306,6 +318,30 @@ def camera_look(W, H, position, forward, vfov=35.0, near=0.1, far=100.0):
     return cam
 
 
+def camera_look_ex(W, H, position, forward, vfov=35.0, near=0.1, far=100.0):
+    """camera + its (non-inverted) projection and view matrices (column-major 16 floats each)."""
+    cam = Camera()
+    proj = np.zeros(16, np.float32); view = np.zeros(16, np.float32)
+    st = lib().rt_camera_look_ex(W, H, _fp(np.asarray(position, np.float32)), _fp(np.asarray(forward, np.float32)), vfov, near, far,
+                                 C.byref(cam), _fp(proj), _fp(view))
+    if st != RT_OK:
+        raise RtError(f"rt_camera_look_ex failed {st}")
+    return cam, proj, view
+
+
+DEFAULT_CAMERA_POSITION = (2.81432, 4.20749, -9.11751)     # MC/Camera.h:19-21, DN/Camera.h:19-20
+DEFAULT_CAMERA_FORWARD = (0.00209191, -0.148299, 0.988941)
+
+
+def denoise_params(**kw):
+    """rt_denoise_params with the DN/Denoiser.h defaults, overridden by keyword."""
+    p = DenoiseParams()
+    lib().rt_denoise_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
 def camera_two_spheres(W, H):
     """The Whitted Style Ray Tracer's Camera{35, 0.1, 100} at (0, 0, 6) looking down -z (WH/Camera.h:17-19, WH/mainloop.cpp:23)."""
     return camera_look(W, H, (0.0, 0.0, 6.0), (0.0, 0.0, -1.0))
@@ -387,6 +423,30 @@ class Context:
         self._check(lib().rt_trace(self.h, n, _fp(org), _fp(dirs), tri.ctypes.data_as(C.POINTER(C.c_int32)),
                                    t.ctypes.data_as(C.POINTER(C.c_double))), "rt_trace")
         return tri, t
+
+    def render_denoised(self, cam, proj, view, frame, params, seed=0, rr=0.8, fetch=True):
+        """One frame of the Denoiser project's Renderer::Render (G-buffer pass, JBF, temporal, pack)."""
+        proj = np.ascontiguousarray(proj, np.float32); view = np.ascontiguousarray(view, np.float32)
+        if fetch:
+            rgba = np.zeros((self.H, self.W), np.uint32)
+            col = np.zeros((self.H, self.W, 4), np.float32)
+            self._check(lib().rt_render_denoised(self.h, C.byref(cam), _fp(proj), _fp(view), frame, seed, rr, C.byref(params),
+                                                 rgba.ctypes.data_as(C.POINTER(C.c_uint32)), _fp(col)), "rt_render_denoised")
+            return rgba, col
+        self._check(lib().rt_render_denoised(self.h, C.byref(cam), _fp(proj), _fp(view), frame, seed, rr, C.byref(params), None, None),
+                    "rt_render_denoised")
+        return None
+
+    def denoise_restart(self):
+        self._check(lib().rt_denoise_restart(self.h), "rt_denoise_restart")
+
+    def gbuffer(self):
+        n = (self.H, self.W)
+        col = np.zeros(n + (4,), np.float32); pos = np.zeros(n + (4,), np.float32); nrm = np.zeros(n + (4,), np.float32)
+        prim = np.zeros(n, np.int32); spa = np.zeros(n + (4,), np.float32)
+        self._check(lib().rt_get_gbuffer(self.h, _fp(col), _fp(pos), _fp(nrm), prim.ctypes.data_as(C.POINTER(C.c_int32)), _fp(spa)),
+                    "rt_get_gbuffer")
+        return dict(color=col, position=pos, normal=nrm, prim=prim, spatial=spa)
 
     def world_trace(self, org, dirs):
         org = np.ascontiguousarray(org, np.float32); dirs = np.ascontiguousarray(dirs, np.float32)

@@ -115,6 +115,17 @@ extern "C" rt_status rt_camera_look(uint32_t W, uint32_t H, const float position
     return RT_OK;
 }
 
+extern "C" rt_status rt_camera_look_ex(uint32_t W, uint32_t H, const float position[3], const float forward[3], float vfov_deg, float zn,
+                                       float zf, rt_camera* out, float* proj_out, float* view_out)
+{
+    rt_status s = rt_camera_look(W, H, position, forward, vfov_deg, zn, zf, out);
+    if (s != RT_OK) return s;
+    const F3 pos{position[0], position[1], position[2]}, fwd{forward[0], forward[1], forward[2]};
+    if (proj_out) store(perspective_fov(vfov_deg * (float)0.01745329251994329576923690768489, (float)W, (float)H, zn, zf), proj_out);
+    if (view_out) store(look_at(pos, add(pos, fwd), F3{0.0f, 1.0f, 0.0f}), view_out);
+    return RT_OK;
+}
+
 extern "C" rt_status rt_camera_default(uint32_t W, uint32_t H, rt_camera* out, float* proj_out, float* view_out)
 {
     // Camera member defaults, MC/Camera.h:19-21 (double literals narrowed to float), Camera{35, 0.1, 100}

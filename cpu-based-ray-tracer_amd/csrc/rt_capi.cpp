@@ -47,6 +47,16 @@ struct rt_ctx {
     rt_stats stats{};
     bool pending_stats = false;
     uint32_t last_flags = 0;
+    // the Denoiser: this frame's G-buffer, filter outputs and the history (previous temporal output, ids, matrices)
+    float4 *d_gb_color = nullptr, *d_gb_pos = nullptr, *d_gb_nrm = nullptr, *d_spatial = nullptr, *d_temporal = nullptr, *d_prev_color = nullptr;
+    int32_t *d_gb_prim = nullptr, *d_prev_prim = nullptr;
+    uint32_t *d_dn_rgba = nullptr;
+    size_t dn_pixels = 0;
+    bool have_prev = false;
+    float prev_proj[16] = {}, prev_view[16] = {};
+    hipEvent_t ev2 = nullptr, ev3 = nullptr;
+    bool pending_denoise = false;
+    bool gb_next = false, gb_clamp = true;   // rt_render_denoised -> rt_render: G-buffer mode
     uint32_t variant = 0;
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
@@ -305,7 +315,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
         if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipStreamCreate"); delete c; return s; }
         c->own_stream = true;
     }
-    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+    if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess || hipEventCreate(&c->ev2) != hipSuccess ||
+        hipEventCreate(&c->ev3) != hipSuccess ||
         hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 256) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
@@ -341,6 +352,10 @@ void rt_destroy(rt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_went); dfree(c->d_wtris);
+    dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
+    dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    if (c->ev3) (void)hipEventDestroy(c->ev3);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -439,6 +454,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
     P.thresh = c->thresh; P.steps = c->steps; P.variant = c->variant;
+    if (c->gb_next) {
+        P.gb_color = c->d_gb_color; P.gb_pos = c->d_gb_pos; P.gb_nrm = c->d_gb_nrm; P.gb_prim = c->d_gb_prim; P.gb_clamp = c->gb_clamp;
+    }
     // small scenes are staged into LDS (one copy per workgroup)
     const size_t lds_bytes = rt_scene_lds_bytes(P);
     const bool lds = (p->flags & RT_RENDER_GLOBAL_SCENE) == 0 && lds_bytes <= kMaxLdsScene;
@@ -480,6 +498,102 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         if (out_accum) HIPC(c, hipMemcpyAsync(out_accum, c->d_accum, npx * 16, hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
     }
+    return RT_OK;
+}
+
+void rt_denoise_params_default(rt_denoise_params* p)
+{
+    if (!p) return;
+    // Denoising::Denoiser members, DN/Denoiser.h:333-358; RayGen_Shader clamps by default (DN/Renderer.h:37)
+    p->jbf_half_size = 7; p->temporal_half_size = 3; p->tolerance = 1.0f; p->current_frame_weighting = 0.2f; p->immediate_clamp = 1;
+    p->sigma_position = 32.0f; p->sigma_color = 0.6f; p->sigma_normal = 0.1f; p->sigma_coplanarity = 0.1f;
+}
+
+rt_status rt_denoise_restart(rt_ctx* c)
+{
+    if (!c) return RT_ERR_INVALID;
+    c->have_prev = false;
+    return RT_OK;
+}
+
+rt_status rt_render_denoised(rt_ctx* c, const rt_camera* cam, const float proj[16], const float view[16], uint32_t frame, uint64_t seed, float rr,
+                             const rt_denoise_params* dp, uint32_t* out_rgba, float* out_color)
+{
+    if (!c || !cam || !proj || !view || !dp) return RT_ERR_INVALID;
+    if (!c->has_scene || c->hdr.n_nodes == 0) { c->err = "no triangle scene uploaded"; return RT_ERR_STATE; }
+    if (!c->d_accum) { c->err = "no viewport (rt_resize)"; return RT_ERR_STATE; }
+    if (c->nranks != 1) { c->err = "the denoiser filters whole frames: rt_resize with nranks == 1"; return RT_ERR_INVALID; }
+    if (frame == 0) { c->err = "frame is 1-based"; return RT_ERR_INVALID; }
+    if (!(rr >= 0.0f && rr < 1.0f)) { c->err = "rr must be in [0, 1)"; return RT_ERR_INVALID; }
+    if (dp->jbf_half_size < 0 || dp->temporal_half_size < 0) { c->err = "negative filter size"; return RT_ERR_INVALID; }
+    HIPC(c, hipSetDevice(c->device));
+    const size_t npx = (size_t)c->W * c->H;
+    if (c->dn_pixels != npx) {
+        HIPC(c, hipStreamSynchronize(c->stream));
+        dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
+        dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba);
+        float4** f4[6] = {&c->d_gb_color, &c->d_gb_pos, &c->d_gb_nrm, &c->d_spatial, &c->d_temporal, &c->d_prev_color};
+        for (float4** q : f4) HIPC(c, hipMalloc((void**)q, npx * sizeof(float4)));
+        HIPC(c, hipMalloc((void**)&c->d_gb_prim, npx * 4));
+        HIPC(c, hipMalloc((void**)&c->d_prev_prim, npx * 4));
+        HIPC(c, hipMalloc((void**)&c->d_dn_rgba, npx * 4));
+        HIPC(c, hipMemsetAsync(c->d_gb_pos, 0, npx * sizeof(float4), c->stream));   // FrameBuffer::Reset value-initializes
+        HIPC(c, hipMemsetAsync(c->d_gb_nrm, 0, npx * sizeof(float4), c->stream));
+        c->dn_pixels = npx;
+        c->have_prev = false;
+    }
+    // 1) the G-buffer frame: the megakernel in GB mode, one sample per pixel
+    rt_render_params rp{frame, 1u, seed, rr, RT_RENDER_EXACT};
+    c->gb_next = true;
+    c->gb_clamp = dp->immediate_clamp != 0;
+    rt_status st = rt_render(c, cam, &rp, nullptr, nullptr);
+    c->gb_next = false;
+    if (st != RT_OK) return st;
+    // 2) joint bilateral + 3) temporal (+ pack)
+    const bool temporal = dp->temporal_half_size > 0;
+    DenoiseParams D{};
+    D.W = (int)c->W; D.H = (int)c->H;
+    D.color = c->d_gb_color; D.pos = c->d_gb_pos; D.nrm = c->d_gb_nrm; D.prim = c->d_gb_prim;
+    D.spatial = dp->jbf_half_size > 0 ? c->d_spatial : c->d_gb_color;
+    D.prev_color = c->d_prev_color; D.prev_prim = c->d_prev_prim;
+    D.temporal = c->d_temporal; D.rgba = c->d_dn_rgba;
+    D.jbf_half = dp->jbf_half_size; D.immediate_clamp = dp->immediate_clamp != 0;
+    D.sigma_position = dp->sigma_position; D.sigma_color = dp->sigma_color; D.sigma_normal = dp->sigma_normal; D.sigma_coplanarity = dp->sigma_coplanarity;
+    D.temporal_half = dp->temporal_half_size; D.tolerance = dp->tolerance; D.weighting = dp->current_frame_weighting;
+    D.have_prev = temporal && c->have_prev;
+    std::memcpy(D.prev_proj, c->prev_proj, sizeof D.prev_proj);
+    std::memcpy(D.prev_view, c->prev_view, sizeof D.prev_view);
+    HIPC(c, hipEventRecord(c->ev2, c->stream));
+    HIPC(c, rt_launch_denoise(D, c->stream));
+    HIPC(c, hipEventRecord(c->ev3, c->stream));
+    c->pending_denoise = true;
+    // the history: previous_frame_g_buffer = g_buffer (its color is the temporal output), DN/Denoiser.h:321-325
+    if (temporal) {
+        HIPC(c, hipMemcpyAsync(c->d_prev_color, c->d_temporal, npx * sizeof(float4), hipMemcpyDeviceToDevice, c->stream));
+        HIPC(c, hipMemcpyAsync(c->d_prev_prim, c->d_gb_prim, npx * 4, hipMemcpyDeviceToDevice, c->stream));
+        std::memcpy(c->prev_proj, proj, sizeof c->prev_proj);
+        std::memcpy(c->prev_view, view, sizeof c->prev_view);
+    }
+    c->have_prev = temporal;   // disabling the filter drops the history (DN/Denoiser.h:237-243)
+    HIPC(c, hipMemcpyAsync(c->d_rgba, c->d_dn_rgba, npx * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (out_rgba) HIPC(c, hipMemcpyAsync(out_rgba, c->d_dn_rgba, npx * 4, hipMemcpyDeviceToHost, c->stream));
+    if (out_color) HIPC(c, hipMemcpyAsync(out_color, c->d_temporal, npx * 16, hipMemcpyDeviceToHost, c->stream));
+    if (out_rgba || out_color) HIPC(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+rt_status rt_get_gbuffer(rt_ctx* c, float* color, float* position, float* normal, int32_t* prim, float* spatial)
+{
+    if (!c) return RT_ERR_INVALID;
+    if (!c->dn_pixels) { c->err = "no denoised frame rendered"; return RT_ERR_STATE; }
+    HIPC(c, hipSetDevice(c->device));
+    const size_t n = c->dn_pixels;
+    if (color) HIPC(c, hipMemcpyAsync(color, c->d_gb_color, n * 16, hipMemcpyDeviceToHost, c->stream));
+    if (position) HIPC(c, hipMemcpyAsync(position, c->d_gb_pos, n * 16, hipMemcpyDeviceToHost, c->stream));
+    if (normal) HIPC(c, hipMemcpyAsync(normal, c->d_gb_nrm, n * 16, hipMemcpyDeviceToHost, c->stream));
+    if (prim) HIPC(c, hipMemcpyAsync(prim, c->d_gb_prim, n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (spatial) HIPC(c, hipMemcpyAsync(spatial, c->d_spatial, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
 
@@ -527,6 +641,13 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
         c->stats.wave_fold = h[8]; c->stats.cycles_service = h[9]; c->stats.cycles_queue = h[10]; c->stats.cycles_trace = h[11];
         c->stats.service_lanes = h[12];
         c->pending_stats = false;
+    }
+    if (c->pending_denoise) {
+        HIPC(c, hipEventSynchronize(c->ev3));
+        float ms = 0.0f;
+        HIPC(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
+        c->stats.last_denoise_ms = ms;
+        c->pending_denoise = false;
     }
     c->stats.block = c->block; c->stats.stack_depth = c->stack_depth;
     *st = c->stats;

@@ -36,6 +36,8 @@ struct KParams {
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
     uint32_t variant;               // A/B of traversal-loop forms (RT_VARIANT; 0 = default)
+    // the Denoiser's G-buffer frame (set => pt_megakernel<..., GB = true>); one sample per pixel
+    float4* gb_color; float4* gb_pos; float4* gb_nrm; int32_t* gb_prim; uint32_t gb_clamp;
 };
 
 // LDS staging of the scene: bytes needed (the kernel's dynamic shared memory when lds == true)
@@ -52,5 +54,18 @@ hipError_t rt_launch_world_trace(const KParams& P, uint32_t n, const float* org,
                                  hipStream_t stream);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);
+
+// the Denoiser's filters (rt_denoise.hip, DN/Denoiser.h): full frames, one device
+struct DenoiseParams {
+    int W, H;
+    const float4* color; const float4* pos; const float4* nrm; const int32_t* prim;   // this frame's G-buffer
+    float4* spatial;                  // joint bilateral output (== color when the filter is off)
+    const float4* prev_color; const int32_t* prev_prim;   // the previous frame (its temporal output)
+    float4* temporal; uint32_t* rgba;
+    int jbf_half; float sigma_position, sigma_color, sigma_normal, sigma_coplanarity; int immediate_clamp;
+    int temporal_half; float tolerance, weighting; int have_prev;
+    float prev_proj[16], prev_view[16];
+};
+hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream);
 
 #endif

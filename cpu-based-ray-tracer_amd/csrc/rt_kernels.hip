@@ -136,7 +136,11 @@ __device__ __forceinline__ V3 sample_hemisphere(V3 n, Rng& g)
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1   // minimum waves per SIMD the register allocation must admit (A/B knob)
 #endif
-template <bool EXACT, bool COUNT, bool LDS>
+// GB: the Denoiser project's frame (DN/Renderer.cpp:101-311): one sample per pixel through the
+// pixel centre (no camera draws, DN/Camera.cpp:133), the camera hit's G-buffer (primitive id, world
+// position, normalized face-forwarded normal) and the path color, clamped when immediate clamping is
+// on, instead of the temporal accumulation.
+template <bool EXACT, bool COUNT, bool LDS, bool GB = false>
 __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
@@ -222,6 +226,20 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 if (ttri >= 0) {
                     mat = f2i(S.tris[4 * ttri].w);
                     emissive = S.mats[2 * mat].w != 0.0f;
+                }
+                if (GB && depth == 0) {
+                    // Renderer::cast_path's G-buffer writes, DN/Renderer.cpp:290-308
+                    if (ttri >= 0) {
+                        const float4 tq1 = S.tris[4 * ttri + 1], tq3 = S.tris[4 * ttri + 3];
+                        const V3 loc = add(ray.o, smul((float)tbest, ray.d));
+                        const V3 N{tq3.x, tq3.y, tq3.z};
+                        const V3 nf = glm_normalize((dot(N, neg(ray.d)) < 0.0f) ? neg(N) : N);
+                        P.gb_prim[local] = f2i(tq1.w);
+                        P.gb_pos[local] = make_float4(loc.x, loc.y, loc.z, 0.0f);
+                        P.gb_nrm[local] = make_float4(nf.x, nf.y, nf.z, 0.0f);
+                    } else {
+                        P.gb_prim[local] = -1;
+                    }
                 }
                 if (depth == 0) {
                     if (ttri < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
@@ -334,9 +352,15 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), rr));
                     }
                 }
+                in_path = false;
+                if (GB) {
+                    // RayGen_Shader, DN/Renderer.cpp:264-275: (clamped) color into the G-buffer
+                    if (P.gb_clamp) L = V3{smin(smax(L.x, 0.0f), 1.0f), smin(smax(L.y, 0.0f), 1.0f), smin(smax(L.z, 0.0f), 1.0f)};
+                    P.gb_color[local] = make_float4(L.x, L.y, L.z, 0.0f);
+                    have_pixel = false;
+                } else {
                 // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
                 acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
-                in_path = false;
                 ++k;
                 if (k == P.n_frames) {
                     const float fr = (float)(P.first_frame + k - 1u);
@@ -345,6 +369,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     P.accum[local] = acc;
                     P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
                     have_pixel = false;
+                }
                 }
             }
             if (new_ray) {
@@ -381,7 +406,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         px = y * P.W + x;
                         have_pixel = true;
                         k = 0;
-                        acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
+                        if (!GB) acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
                     }
                 }
             }
@@ -390,10 +415,16 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
             g.start(P.seed, px, P.first_frame + k);
-            const float ux = g.next();
-            const float uy = g.next();
-            float cx = ((float)x + ux) / (float)P.W;
-            float cy = ((float)y + uy) / (float)P.H;
+            float cx, cy;
+            if (GB) {   // centre of the pixel, DN/Camera.cpp:133
+                cx = ((float)x + 0.5f) / (float)P.W;
+                cy = ((float)y + 0.5f) / (float)P.H;
+            } else {
+                const float ux = g.next();
+                const float uy = g.next();
+                cx = ((float)x + ux) / (float)P.W;
+                cy = ((float)y + uy) / (float)P.H;
+            }
             cx = cx * 2.0f - 1.0f;
             cy = cy * 2.0f - 1.0f;
             float tg[4];
@@ -526,7 +557,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     }
 }
 
-#define RT_INST(E, C, L) template __global__ void pt_megakernel<E, C, L>(KParams);
+#define RT_INST(E, C, L) template __global__ void pt_megakernel<E, C, L, false>(KParams);
+template __global__ void pt_megakernel<true, false, true, true>(KParams);
+template __global__ void pt_megakernel<true, false, false, true>(KParams);
 RT_INST(true, false, true) RT_INST(true, true, true) RT_INST(false, false, true) RT_INST(false, true, true)
 RT_INST(true, false, false) RT_INST(true, true, false) RT_INST(false, false, false) RT_INST(false, true, false)
 
@@ -555,6 +588,11 @@ size_t rt_scene_lds_bytes(const KParams& P)
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream)
 {
     const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
+    if (P.gb_color) {   // the Denoiser's G-buffer frame (EXACT, no counters)
+        if (lds) hipLaunchKernelGGL((pt_megakernel<true, false, true, true>), dim3(grid), dim3(block), sh, stream, P);
+        else hipLaunchKernelGGL((pt_megakernel<true, false, false, true>), dim3(grid), dim3(block), sh, stream, P);
+        return hipGetLastError();
+    }
     const int sel = (exact ? 4 : 0) | (count ? 2 : 0) | (lds ? 1 : 0);
     switch (sel) {
         case 7: return launch_one<true, true, true>(P, grid, block, sh, stream);

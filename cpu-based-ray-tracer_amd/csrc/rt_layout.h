@@ -15,7 +15,8 @@
 //            so a stackless walk visits exactly the nodes the reference's recursion visits
 //            (BVH::traverse_BVH_from_node, MC/BVH.h:82-101).
 //  tris    : 4 x float4 per triangle, in DFS leaf order (slot == flattened leaf index)
-//              q0 = (a.xyz, bits(material)), q1 = (e1 = b-a, 0), q2 = (e2 = c-a, 0), q3 = (n.xyz, 0)
+//              q0 = (a.xyz, bits(material)), q1 = (e1 = b-a, bits(primitive id)), q2 = (e2 = c-a, 0), q3 = (n.xyz, 0)
+//            (primitive id: 1 + creation index over all meshes, the Denoiser's G-buffer id, DN/TriangleMesh.h:54-62)
 //            (Moller-Trumbore reads q0..q2 = 48 B; shading reads q3)
 //  mats    : 2 x float4 per material: (brdf = albedo/PI, emitting), (emission, 0)
 //  lnodes  : light-mesh BVH for area sampling (BVH::Sampling_from_node, MC/BVH.h:114-129):

@@ -45,6 +45,7 @@ struct Tri {
     float area;
     Box box;
     int mesh;
+    int id;   // primitive id: 1 + creation index over all meshes (DN/TriangleMesh.h:54-62, DN/Renderer.cpp:36-43)
 };
 
 // A built (unflattened) binary tree; leaves reference an item id.
@@ -298,6 +299,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     std::vector<int> mesh_root(nm, -1);
     std::vector<Box> mesh_box(nm);
     std::vector<float> mesh_area(nm, 0.0f);
+    int id_count = 1;
     for (size_t mi = 0; mi < nm; ++mi) {
         const auto& raw = meshes_[mi].raw;
         const size_t nt = raw.size() / 9;
@@ -318,7 +320,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
                 rmax = F3{std::max(rmax.x, v[j].x), std::max(rmax.y, v[j].y), std::max(rmax.z, v[j].z)};
             }
             Tri tr;
-            tr.a = v[0]; tr.b = v[1]; tr.c = v[2]; tr.mesh = (int)mi;
+            tr.a = v[0]; tr.b = v[1]; tr.c = v[2]; tr.mesh = (int)mi; tr.id = id_count++;
             const F3 cp = cross(sub(tr.b, tr.a), sub(tr.c, tr.a));
             tr.area = 0.5f * std::sqrt(dot(cp, cp));
             const float l2 = cp.x * cp.x + cp.y * cp.y + cp.z * cp.z;   // Whitted::normalize (zero-safe)
@@ -408,7 +410,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         const F3 e1 = sub(t.b, t.a), e2 = sub(t.c, t.a);
         float* q = &out.tris[16 * (size_t)s];
         q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = bits_as_float(t.mesh);   // material id == mesh id
-        q[4] = e1.x; q[5] = e1.y; q[6] = e1.z; q[7] = 0.0f;
+        q[4] = e1.x; q[5] = e1.y; q[6] = e1.z; q[7] = bits_as_float(t.id);
         q[8] = e2.x; q[9] = e2.y; q[10] = e2.z; q[11] = 0.0f;
         q[12] = t.n.x; q[13] = t.n.y; q[14] = t.n.z; q[15] = 0.0f;
         float* d = &out.dbg_tri_f[13 * (size_t)s];

@@ -18,6 +18,8 @@
  *   rt_trace                              Renderer::ray_BVH_intersection_record             MC/Renderer.h:88-91
  *   rt_render + RT_RENDER_WHITTED         BVH Ray Tracer Renderer::Render / cast_Whitted_ray   BV/Renderer.cpp:69-233
  *   rt_scene_add_bvh_tracer_scene         BVH Ray Tracer Renderer::Renderer()                  BV/Renderer.cpp:26-43
+ *   rt_render_denoised                    Denoiser project Renderer::Render (G-buffer, JBF,    DN/Renderer.cpp:101-311,
+ *                                         temporal filter)                                   DN/Denoiser.h:133-328
  *   rt_scene_add_world_sphere / _mesh     Whitted Style Ray Tracer Sphere / TriangleMesh + World::Add
  *                                         (WH/Sphere.h:16-75, WH/TriangleMesh.h:47-155, WH/World.h:37-45)
  *   rt_scene_add_two_spheres_scene        Whitted Style Ray Tracer Renderer::Renderer()       WH/Renderer.cpp:27-49
@@ -118,6 +120,10 @@ rt_status rt_camera_default(uint32_t width, uint32_t height, rt_camera* out, flo
 /* a camera at `position` looking along `forward` (up = +y), glm::lookAt / perspectiveFov */
 rt_status rt_camera_look(uint32_t width, uint32_t height, const float position[3], const float forward[3], float vfov_deg,
                          float near_clip, float far_clip, rt_camera* out);
+/* the same plus the (non-inverted) projection and view matrices (16 floats each, may be NULL), which
+ * the Denoiser's temporal reprojection uses (DN/Renderer.cpp:254-256) */
+rt_status rt_camera_look_ex(uint32_t width, uint32_t height, const float position[3], const float forward[3], float vfov_deg,
+                            float near_clip, float far_clip, rt_camera* out, float* proj, float* view);
 
 /* ------------------------------------------------------------------ device context */
 typedef struct {
@@ -174,8 +180,34 @@ typedef struct {
     /* RT_RENDER_COUNT: wave-level fold iterations; wave cycles (s_memtime) spent in service,
      * work-queue + camera-ray, and traversal rounds; lanes served per service round (sum) */
     uint64_t wave_fold, cycles_service, cycles_queue, cycles_trace, service_lanes;
+    float last_denoise_ms;    /* rt_render_denoised: the joint bilateral + temporal kernels (HIP events) */
 } rt_stats;
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
+
+/* ------------------------------------------------------------------ the Denoiser (DN/ = Denoiser/8599RayTracerGUI/src/)
+ * One call = one Renderer::Render of the Denoiser project (DN/Renderer.cpp:101-283): a 1-spp path-traced
+ * frame through the pixel centres that records the G-buffer (DN/Renderer.cpp:285-311), the joint
+ * bilateral filter and the temporal filter of DN/Denoiser.h, and the RGBA8 pack.  Full frames on one
+ * device (rt_resize with nranks == 1).  The history (previous frame's output, primitive ids and
+ * matrices) lives in the context; rt_denoise_restart drops it (Renderer::RestartTemporal, DN/Renderer.h:74-77). */
+typedef struct {
+    int32_t jbf_half_size;            /* 0: joint bilateral filter off; the UI's 15/33/65 px kernels are 3/16/32 */
+    int32_t temporal_half_size;       /* 0: temporal filter off; the UI's 7/15/33 px kernels are 3/7/16 */
+    float tolerance;                  /* history clamp, in deviations (1, 2, 3) */
+    float current_frame_weighting;    /* 0.05 / 0.1 / 0.2 / 0.5 */
+    int32_t immediate_clamp;          /* clamp each frame's color to [0,1] before filtering (default 1) */
+    float sigma_position, sigma_color, sigma_normal, sigma_coplanarity;   /* 32, 0.6, 0.1, 0.1 */
+} rt_denoise_params;
+/* DN/Denoiser.h member defaults (JBF half size 7, temporal 3, tolerance 1, weighting 0.2, sigmas) */
+void rt_denoise_params_default(rt_denoise_params* p);
+/* proj/view: this frame's camera matrices (rt_camera_look_ex); frame: the RNG frame index (1-based);
+ * out_rgba (W x H u32) / out_color (W x H x 4 f32: the temporal output) may be NULL */
+rt_status rt_render_denoised(rt_ctx* ctx, const rt_camera* cam, const float proj[16], const float view[16], uint32_t frame, uint64_t seed,
+                             float rr, const rt_denoise_params* p, uint32_t* out_rgba, float* out_color);
+rt_status rt_denoise_restart(rt_ctx* ctx);
+/* the last denoised frame's buffers (W x H each; any pointer may be NULL): G-buffer color / world
+ * position / normal (4 floats per pixel), primitive id (-1: primary ray missed), joint bilateral output */
+rt_status rt_get_gbuffer(rt_ctx* ctx, float* color, float* position, float* normal, int32_t* prim, float* spatial);
 
 /* closest hit of n rays (host arrays; tri = flattened triangle slot or -1, t = double distance) */
 rt_status rt_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t);

@@ -8,6 +8,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
 
     python oracle/gen_golden.py            # all fixtures
     python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
+    python oracle/gen_golden.py dn         # only the Denoiser project fixtures
     python oracle/gen_golden.py c1         # only the C1 (Whitted two-sphere world) fixtures
     python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
@@ -489,9 +490,57 @@ def gen_c1(rng):
     np.savez_compressed(os.path.join(GOLDEN, "c1_spheres.npz"), **out)
 
 
+# ------------------------------------------------------------------ the Denoiser project
+HARNESS_DN = os.path.join(HERE, "_ref", "ref_denoiser")
+DN_DIR = os.path.join(REF, "Denoiser", "8599RayTracerGUI", "src", "cornellbox")
+# (name, W, H, frames, seed, step_x, jbf_half, temporal_half, tolerance, weighting, immediate_clamp)
+DN_CASES = [("full", 96, 72, 4, 0, 0.05, 3, 3, 1.0, 0.2, 1),
+            ("temporal", 96, 72, 3, 5, 0.08, 0, 7, 2.0, 0.1, 1),
+            ("jbf16", 64, 48, 2, 9, 0.0, 16, 0, 1.0, 0.2, 0)]
+
+
+def gen_dn():
+    """Frames of the Denoiser project through the reference's own Denoising::Denoiser (DN/Denoiser.h,
+    compiled as is) and its DN/ geometry + camera code (shading glue restated, oracle/ref/ref_denoiser.cpp)."""
+    out = {}
+    for (name, W, H, n, seed, step, jh, th, tol, wgt, clamp) in DN_CASES:
+        r = subprocess.run([HARNESS_DN, "frames", DN_DIR, str(W), str(H), str(n), str(seed), repr(step), str(jh), str(th), repr(tol),
+                            repr(wgt), str(clamp), str(os.cpu_count() or 8), tmp("dn.bin")], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"ref_denoiser failed: {r.stderr}")
+        print(" ", r.stdout.strip())
+        b = np.fromfile(tmp("dn.bin"), np.uint8)
+        npx = W * H
+        off = 0
+
+        def take(dt, count):
+            nonlocal off
+            nb = np.dtype(dt).itemsize * count
+            v = b[off:off + nb].view(dt)
+            off += nb
+            return v
+        for k in range(n):
+            key = f"{name}_f{k + 1}"
+            out[f"{key}_color"] = take("<f4", 3 * npx).reshape(H, W, 3)
+            out[f"{key}_pos"] = take("<f4", 3 * npx).reshape(H, W, 3)
+            out[f"{key}_nrm"] = take("<f4", 3 * npx).reshape(H, W, 3)
+            out[f"{key}_contrib"] = take("<i4", npx).reshape(H, W)
+            out[f"{key}_prim"] = take("<i4", npx).reshape(H, W)
+            out[f"{key}_proj"] = take("<f4", 16)
+            out[f"{key}_view"] = take("<f4", 16)
+            out[f"{key}_campos"] = take("<f4", 3)
+            out[f"{key}_spatial"] = take("<f4", 3 * npx).reshape(H, W, 3)
+            out[f"{key}_temporal"] = take("<f4", 3 * npx).reshape(H, W, 3)
+            out[f"{key}_rgba"] = take("<u4", npx).reshape(H, W)
+        assert off == b.size
+        out[f"{name}_params"] = np.array([W, H, n, seed, jh, th, clamp], np.int64)
+        out[f"{name}_fparams"] = np.array([step, tol, wgt], np.float32)
+    np.savez_compressed(os.path.join(GOLDEN, "denoiser.npz"), **out)
+
+
 def main():
     global TMP
-    if not os.path.exists(HARNESS) or not os.path.exists(HARNESS_BV) or not os.path.exists(HARNESS_WH):
+    if not all(os.path.exists(h) for h in (HARNESS, HARNESS_BV, HARNESS_WH, HARNESS_DN)):
         subprocess.check_call(["make", "-C", HERE, "ref"])
     os.makedirs(GOLDEN, exist_ok=True)
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
@@ -515,6 +564,8 @@ def main():
             gen_bvh_images()
         if only in ("all", "c1"):
             gen_c1(np.random.default_rng(20261017))
+        if only in ("all", "dn"):
+            gen_dn()
         if only in ("all", "c5"):
             gen_c5(np.random.default_rng(20261016))
     print("golden fixtures written to", GOLDEN)

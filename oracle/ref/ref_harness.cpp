@@ -48,70 +48,7 @@
 #undef private
 #include "../philox.h"
 
-// ---------------------------------------------------------------------------------------------
-// RNG injection
-// ---------------------------------------------------------------------------------------------
-struct MTLayout { std::mt19937::result_type x[624]; size_t p; };
-static_assert(sizeof(MTLayout) == sizeof(std::mt19937), "unexpected libstdc++ mt19937 layout");
-
-static uint32_t mt_untemper(uint32_t y)
-{
-    // inverse of std::mt19937 tempering (u=11,d=0xffffffff,s=7,b=0x9d2c5680,t=15,c=0xefc60000,l=18)
-    uint32_t x = y;
-    x = y ^ (y >> 18);
-    { uint32_t z = x; uint32_t r = z; for (int i = 0; i < 3; ++i) r = z ^ ((r << 15) & 0xefc60000u); x = r; }
-    { uint32_t z = x; uint32_t r = z; for (int i = 0; i < 5; ++i) r = z ^ ((r << 7) & 0x9d2c5680u); x = r; }
-    { uint32_t z = x; uint32_t r = z; for (int i = 0; i < 3; ++i) r = z ^ (r >> 11); x = r; }
-    return x;
-}
-
-static void check_layout_once()
-{
-    std::mt19937 e;
-    MTLayout l;
-    for (int i = 0; i < 624; ++i) l.x[i] = mt_untemper(0x1000u + (uint32_t)i * 7919u);
-    l.p = 0;
-    std::memcpy((void*)&e, &l, sizeof l);
-    for (int i = 0; i < 624; ++i) {
-        uint32_t v = (uint32_t)e();
-        if (v != 0x1000u + (uint32_t)i * 7919u) { fprintf(stderr, "mt19937 injection self-check failed at %d\n", i); exit(3); }
-    }
-}
-
-struct Injector {
-    uint64_t seed = 0;
-    uint32_t pixel = 0, frame = 0;
-    uint32_t filled = 0;
-    std::mt19937::result_type x0 = 0;
-    void start(uint64_t s, uint32_t px, uint32_t fr, uint32_t n)
-    {
-        seed = s; pixel = px; frame = fr;
-        MTLayout l;
-        if (n > 624) n = 624;
-        for (uint32_t i = 0; i < n; ++i) l.x[i] = mt_untemper(oracle_rng_u32(seed, pixel, frame, i));
-        // past the filled prefix: all-ones draws (Float()==1.0f ends the path at the next RR test);
-        // a path that still exhausts the engine triggers a twist, detected through x[0] in used()
-        for (uint32_t i = n; i < 624; ++i) l.x[i] = mt_untemper(0xFFFFFFFFu);
-        l.p = 0;
-        filled = n;
-        x0 = l.x[0];
-        std::memcpy((void*)&Walnut::Random::s_RandomEngine, &l, sizeof l);
-    }
-    // number of draws consumed; 0xFFFFFFFF if the engine twisted (more than 624 draws)
-    uint32_t used() const
-    {
-        MTLayout l;
-        std::memcpy(&l, (const void*)&Walnut::Random::s_RandomEngine, sizeof l);
-        if (l.x[0] != x0) return 0xFFFFFFFFu;
-        return (uint32_t)l.p;
-    }
-};
-static thread_local Injector g_inj;
-
-static void set_msvc_distribution()
-{
-    Walnut::Random::s_Distribution = std::uniform_int_distribution<std::mt19937::result_type>(0u, 0xFFFFFFFFu);
-}
+#include "mt_inject.h"
 
 // raw injection of an explicit list of u32 draws (unit cases)
 static void inject_list(const std::vector<uint32_t>& v)

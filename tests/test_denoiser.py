@@ -1,0 +1,115 @@
+"""The reference's Denoiser project (DN/ = "Denoiser/8599RayTracerGUI/src/"): a
+1-spp path-traced Cornell-box frame through the pixel centres that records a G-buffer
+(DN/Renderer.cpp:285-311), the joint bilateral filter and the temporal filter of DN/Denoiser.h, and the
+RGBA8 pack (DN/Renderer.cpp:101-283) -- on the GPU (megakernel GB mode + rt_denoise.hip) against
+golden frames from oracle/_ref/ref_denoiser (the reference's Denoising::Denoiser compiled as it is, its
+DN/ geometry and camera code, the path-tracing glue restated; oracle/gen_golden.py `dn`).  The camera
+moves between frames, so the temporal reprojection is exercised.
+
+Tolerances: the G-buffer (color, position, normal, primitive id) and every output of a pipeline
+without the joint bilateral filter are bit-exact.  The filter's weights call expf/acosf (glibc in the
+reference, double-evaluated and rounded on the device): its outputs are held to 2e-6 absolute and
+the RGBA8 frames to one level on at most 0.5 % of pixels."""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _rt import rt
+
+FWD = rt.DEFAULT_CAMERA_FORWARD
+JBF_ABS_TOL = 2e-6
+
+
+@pytest.fixture(scope="module")
+def fixture():
+    return np.load(os.path.join(O.GOLDEN, "denoiser.npz"))
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+def cases(z):
+    for name in ("full", "temporal", "jbf16"):
+        W, H, n, seed, jh, th, clamp = (int(v) for v in z[f"{name}_params"])
+        step, tol, wgt = (float(v) for v in z[f"{name}_fparams"])
+        yield name, W, H, n, seed, jh, th, clamp, tol, wgt
+
+
+def test_camera_matrices_match_reference(fixture):
+    for name, W, H, n, *_ in cases(fixture):
+        for k in range(n):
+            key = f"{name}_f{k + 1}"
+            _, proj, view = rt.camera_look_ex(W, H, fixture[f"{key}_campos"], FWD)
+            assert np.array_equal(bits(proj), bits(fixture[f"{key}_proj"])), key
+            assert np.array_equal(bits(view), bits(fixture[f"{key}_view"])), key
+
+
+def test_params_defaults_are_the_reference_members():
+    p = rt.denoise_params()
+    assert (p.jbf_half_size, p.temporal_half_size, p.immediate_clamp) == (7, 3, 1)
+    assert np.float32(p.tolerance) == np.float32(1.0) and np.float32(p.current_frame_weighting) == np.float32(0.2)
+    assert [np.float32(v) for v in (p.sigma_position, p.sigma_color, p.sigma_normal, p.sigma_coplanarity)] == \
+           [np.float32(32.0), np.float32(0.6), np.float32(0.1), np.float32(0.1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["full", "temporal", "jbf16"])
+def test_denoised_frames(fixture, case):
+    z = fixture
+    name, W, H, n, seed, jh, th, clamp, tol, wgt = next(c for c in cases(z) if c[0] == case)
+    ctx = rt.Context(0)
+    try:
+        ctx.upload(rt.Scene.cornell())
+        ctx.resize(W, H)
+        params = rt.denoise_params(jbf_half_size=jh, temporal_half_size=th, tolerance=tol, current_frame_weighting=wgt, immediate_clamp=clamp)
+        for k in range(n):
+            key = f"{name}_f{k + 1}"
+            cam, proj, view = rt.camera_look_ex(W, H, z[f"{key}_campos"], FWD)
+            rgba, out = ctx.render_denoised(cam, proj, view, k + 1, params, seed=seed)
+            gb = ctx.gbuffer()
+            prim = z[f"{key}_prim"]
+            hit = prim != -1
+            assert np.array_equal(gb["prim"], prim), key
+            assert np.array_equal(hit.astype(np.int32), z[f"{key}_contrib"]), key
+            assert np.array_equal(bits(gb["color"][..., :3]), bits(z[f"{key}_color"])), key
+            assert np.array_equal(bits(gb["position"][..., :3][hit]), bits(z[f"{key}_pos"][hit])), key
+            assert np.array_equal(bits(gb["normal"][..., :3][hit]), bits(z[f"{key}_nrm"][hit])), key
+            if jh > 0:
+                d = np.abs(gb["spatial"][..., :3].astype(np.float64) - z[f"{key}_spatial"])
+                assert d.max() <= JBF_ABS_TOL, (key, d.max())
+                d = np.abs(out[..., :3].astype(np.float64) - z[f"{key}_temporal"])
+                assert d.max() <= JBF_ABS_TOL, (key, d.max())
+                diff = rgba != z[f"{key}_rgba"]
+                assert diff.mean() <= 0.005, (key, diff.mean())
+                lv = np.abs(rgba.view(np.uint8).astype(np.int32) - z[f"{key}_rgba"].view(np.uint8).astype(np.int32))
+                assert lv.max() <= 1, key
+            else:
+                assert np.array_equal(bits(out[..., :3]), bits(z[f"{key}_temporal"])), key
+                assert np.array_equal(rgba, z[f"{key}_rgba"]), key
+        st = ctx.stats()
+        assert st.last_denoise_ms > 0.0
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_restart_drops_the_history(fixture):
+    """Renderer::RestartTemporal (DN/Renderer.h:74-77): after a restart the next frame is not blended."""
+    z = fixture
+    name, W, H, n, seed, jh, th, clamp, tol, wgt = next(c for c in cases(z) if c[0] == "temporal")
+    ctx = rt.Context(0)
+    try:
+        ctx.upload(rt.Scene.cornell())
+        ctx.resize(W, H)
+        params = rt.denoise_params(jbf_half_size=0, temporal_half_size=th, tolerance=tol, current_frame_weighting=wgt)
+        cam, proj, view = rt.camera_look_ex(W, H, z[f"{name}_f1_campos"], FWD)
+        ctx.render_denoised(cam, proj, view, 1, params, seed=seed)
+        ctx.denoise_restart()
+        cam, proj, view = rt.camera_look_ex(W, H, z[f"{name}_f2_campos"], FWD)
+        _, out = ctx.render_denoised(cam, proj, view, 2, params, seed=seed)
+        assert np.array_equal(bits(out[..., :3]), bits(z[f"{name}_f2_color"]))   # == this frame's G-buffer color
+    finally:
+        ctx.close()

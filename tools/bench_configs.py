@@ -44,13 +44,35 @@ def run(ctx, cam, W, H, spp, reps, **kw):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="C1,C2,C3,C4,C5")
+    ap.add_argument("--configs", default="C1,C2,C3,C4,C5,DN15,DN33,DN65")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--c5-spp", type=int, default=64)
     ap.add_argument("--fast", action="store_true")
     args = ap.parse_args()
     bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
     for c in args.configs.split(","):
+        if c.startswith("DN"):
+            # the Denoiser project at 1920x1080: G-buffer frame + joint bilateral filter of the UI's
+            # 15/33/65-pixel kernel (half sizes 3/16/32) + temporal filter (7-pixel kernel), per frame
+            W, H = 1920, 1080
+            half = {"DN15": 3, "DN33": 16, "DN65": 32}[c]
+            ctx = rt.Context(0)
+            ctx.upload(rt.Scene.cornell())
+            ctx.resize(W, H)
+            params = rt.denoise_params(jbf_half_size=half, temporal_half_size=3)
+            gms, dms = [], []
+            for f in range(1, 2 + args.reps):
+                cam, proj, view = rt.camera_look_ex(W, H, rt.DEFAULT_CAMERA_POSITION, rt.DEFAULT_CAMERA_FORWARD)
+                ctx.render_denoised(cam, proj, view, f, params, fetch=False)
+                st = ctx.stats()
+                if f > 1:
+                    gms.append(st.last_kernel_ms); dms.append(st.last_denoise_ms)
+            print(json.dumps({"config": c, "width": W, "height": H, "jbf_half_size": half, "temporal_half_size": 3,
+                              "gbuffer_ms": round(float(np.median(gms)), 3), "denoise_ms": round(float(np.median(dms)), 3),
+                              "frame_ms": round(float(np.median(gms)) + float(np.median(dms)), 3),
+                              "jbf_taps_per_s": round(W * H * (2 * half + 1) ** 2 / (float(np.median(dms)) / 1e3) / 1e9, 2)}), flush=True)
+            ctx.close()
+            continue
         ctx = rt.Context(0)
         kw = {}
         if c == "C1":
