@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""The reference renderers on this host's CPU cores, per configuration (the CPU side of
+tools/bench_configs.py): each harness under oracle/_ref/ runs the reference's own compiled geometry,
+material, camera (and, for the Denoiser, filter) code with the shading glue restated (oracle/ref/).
+Bounded samples (a few seconds each); prints one JSON line per configuration.
+
+    python tools/cpu_reference_configs.py [--threads 16]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+REF = os.path.join(REPO, "oracle", "_ref")
+
+
+def timed(cmd):
+    t0 = time.perf_counter()
+    subprocess.run(cmd, check=True, capture_output=True)
+    return time.perf_counter() - t0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--threads", type=int, default=min(16, os.cpu_count() or 1))
+    args = ap.parse_args()
+    T = str(args.threads)
+    import _oracle as O
+    from _rt import rt
+    tmp = tempfile.mkdtemp(prefix="rt_cpuref_")
+    out = [os.path.join(tmp, x) for x in ("a", "r", "s")]
+    # the Cornell meshes (and the C5 bunny) as OBJ files for the harnesses
+    for (name, raw, _, _) in O.cornell_meshes():
+        rt.write_obj(os.path.join(tmp, name + ".obj"), raw)
+    bunny = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
+    rt.write_obj(os.path.join(tmp, "c5_bunny.obj"), rt.c5_mesh(bunny["raw_bunny"]))
+    bvdir = os.path.join(tmp, "bv")
+    os.makedirs(bvdir)
+    rt.write_obj(os.path.join(bvdir, "bunny.obj"), bunny["raw_bunny"])
+    rt.write_obj(os.path.join(bvdir, "teapot.obj"), bunny["raw_teapot"])
+    lines = []
+    # C1: the Whitted world, 640x480, one frame
+    dt = timed([os.path.join(REF, "ref_whitted_spheres"), "image", "640", "480", "1", T] + out)
+    lines.append({"config": "C1", "samples": 640 * 480, "seconds": dt})
+    # C2 / C4: Cornell MC at reduced spp (frames are i.i.d., time is linear in spp)
+    for c, (W, H, spp) in (("C2", (784, 784, 4)), ("C4", (1920, 1080, 2))):
+        dt = timed([os.path.join(REF, "ref_harness"), "image", tmp, "", str(W), str(H), str(spp), "0", "0.8", T] + out)
+        lines.append({"config": c, "samples": W * H * spp, "seconds": dt})
+    # C3: the BVH Ray Tracer, 1280x960, one frame (deterministic: every frame costs the same)
+    dt = timed([os.path.join(REF, "ref_whitted_bvh"), "image", os.path.join(bvdir, "bunny.obj"), os.path.join(bvdir, "teapot.obj"),
+                "1280", "960", "1", T] + out)
+    lines.append({"config": "C3", "samples": 1280 * 960, "seconds": dt, "note": "includes the OBJ load + BVH build"})
+    # C5: Cornell + 79,488-triangle bunny at 960x540, 1 spp (plus the scene build)
+    dt = timed([os.path.join(REF, "ref_harness"), "image", tmp, os.path.join(tmp, "c5_bunny.obj"), "960", "540", "1", "0", "0.8", T] + out)
+    lines.append({"config": "C5", "samples": 960 * 540, "seconds": dt, "note": "960x540x1, includes the OBJ load + BVH build"})
+    # the Denoiser project: 480x270, 2 frames, joint bilateral 65 px (half 32) + temporal
+    dt = timed([os.path.join(REF, "ref_denoiser"), "frames", tmp, "480", "270", "2", "0", "0.05", "32", "3", "1.0", "0.2", "1", T,
+                os.path.join(tmp, "dn.bin")])
+    lines.append({"config": "DN65", "samples": 480 * 270 * 2, "seconds": dt, "note": "480x270, 2 frames; per-frame cost scales with W*H"})
+    for d in lines:
+        d["threads"] = args.threads
+        d["msamples_per_s"] = round(d["samples"] / d["seconds"] / 1e6, 4)
+        d["seconds"] = round(d["seconds"], 3)
+        print(json.dumps(d), flush=True)
+
+
+if __name__ == "__main__":
+    main()
