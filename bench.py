@@ -139,12 +139,15 @@ def main():
     gat = rtdist.ImageGather(W, H, args.band, rank, world, dev)
     assert gat.n_local == ctx.local_rows
     kernel_ms = []
+    launch_info = {}
 
     def step():
         ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not args.fast, fetch=False)
         ctx.copy_rgba_to_device(gat.send.data_ptr())   # this rank's rows, on the shared stream
         gat.gather()                                    # RCCL all-gather + reassembly on rank 0
-        kernel_ms.append(ctx.stats().last_kernel_ms)
+        st = ctx.stats()
+        kernel_ms.append(st.last_kernel_ms)
+        launch_info.update(passes=st.n_passes, chunks=st.n_chunks)
 
     for _ in range(args.warmup):
         step()
@@ -169,20 +172,25 @@ def main():
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
 
-    # roofline of the megakernel on this rank: algorithmic bytes per launch / mean launch time
+    # roofline of the megakernel on this rank: algorithmic bytes per launch / mean launch time.  A step
+    # is `passes` launches over consecutive frame ranges (each followed by the in-order finalize of its
+    # frame chunks, included in the HIP-event time); per launch = per step / passes.
     local_samples = gat.n_local * W * spp
-    k_s = float(np.mean(kernel_ms)) / 1e3 if kernel_ms else float("nan")
-    achieved = BYTES_PER_SAMPLE * local_samples / k_s / 1e9
+    passes = max(1, int(launch_info.get("passes", 1)))
+    k_s = float(np.mean(kernel_ms)) / 1e3 / passes if kernel_ms else float("nan")
+    per_launch = local_samples / passes
+    achieved = BYTES_PER_SAMPLE * per_launch / k_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "pt_megakernel", "kernel_ms": round(k_s * 1e3, 3),
-            "bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "samples_per_launch": local_samples,
-            "gsamples_per_s_kernel": round(local_samples / k_s / 1e9, 4)}
+            "bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "samples_per_launch": int(per_launch),
+            "launches_per_step": passes, "frame_chunks": int(launch_info.get("chunks", 1)),
+            "gsamples_per_s_kernel": round(per_launch / k_s / 1e9, 4)}
     prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(prof):
         try:
             pm = json.load(open(prof))
-            key = f"{W}x{H}x{spp}_{'fast' if args.fast else 'exact'}_n{world}"
+            key = f"{W}x{H}x{spp}_{'fast' if args.fast else 'exact'}_n{world}_p{passes}"
             if key in pm:
                 roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
         except Exception:

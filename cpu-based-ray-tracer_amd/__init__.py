@@ -48,7 +48,8 @@ class Stats(C.Structure):
                 ("stack_depth", C.c_uint32), ("wave_rounds", C.c_uint64), ("wave_steps", C.c_uint64),
                 ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64), ("wave_fold", C.c_uint64),
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
-                ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float)]
+                ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
+                ("n_passes", C.c_uint32)]
 
 
 class DenoiseParams(C.Structure):

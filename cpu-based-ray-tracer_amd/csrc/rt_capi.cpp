@@ -58,6 +58,12 @@ struct rt_ctx {
     bool pending_denoise = false;
     bool gb_next = false, gb_clamp = true;   // rt_render_denoised -> rt_render: G-buffer mode
     uint32_t variant = 0;
+    // frame chunking (KParams::n_chunks): split when a launch has fewer than min_px_per_lane pixels
+    // per lane, into about items_per_lane items per lane (RT_CHUNKS forces a count)
+    uint32_t force_chunks = 0, items_per_lane = 32, min_px_per_lane = 32;
+    uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch (RT_LBUF_BUDGET_MB); C4 needs 20 GB of 288
+    float* d_lbuf = nullptr;
+    size_t lbuf_floats = 0;
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
 
@@ -306,6 +312,10 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_VARIANT")) c->variant = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = std::getenv("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
     if (cfg && cfg->stream) {
@@ -353,7 +363,7 @@ void rt_destroy(rt_ctx* c)
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
-    dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba);
+    dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev3) (void)hipEventDestroy(c->ev3);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
@@ -475,9 +485,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
-    HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 256, c->stream));
+    const uint64_t px_local = (uint64_t)c->local_rows * c->W;
+    const uint64_t items_px = P.n_items;   // 8x8-tile-padded pixel items
     c->last_flags = p->flags;
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 256, c->stream));
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
         if (whitted && c->hdr.n_went > 0) {
@@ -485,7 +496,55 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         } else if (whitted) {
             HIPC(c, rt_launch_whitted(P, count, c->stream, &grid));
         } else {
-            HIPC(c, rt_launch_megakernel(P, exact, count, lds, grid, c->block, c->stream));
+            // Frame chunks: a lane renders one work item's frames in order, so a launch with few items
+            // per lane waits on the costliest pixels' sequential frames (the tail; a row band of a
+            // multi-GPU frame is 1 pixel per lane).  Each pixel's frames are split into chunks, about
+            // items_per_lane items per lane: chunk 0 accumulates, later chunks park their samples
+            // (12 B each) for the in-order finalize pass.  The parked samples of one launch are capped
+            // by lbuf_budget; a longer render runs as several passes over consecutive frame ranges
+            // (first_frame continues the accumulation, so passes are exact too).
+            const uint64_t lanes = (uint64_t)grid * c->block;
+            uint32_t want = 1;
+            if (!c->gb_next && p->n_frames > 1 && px_local > 0) {
+                if (c->force_chunks) want = std::min(c->force_chunks, p->n_frames);
+                else if (px_local < (uint64_t)c->min_px_per_lane * lanes)
+                    want = (uint32_t)std::min<uint64_t>(p->n_frames, ((uint64_t)c->items_per_lane * lanes + px_local - 1) / px_local);
+            }
+            uint32_t passes = 1;
+            if (want > 1) {
+                const uint64_t bytes = px_local * (uint64_t)p->n_frames * 12ull;
+                passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
+            }
+            uint32_t done = 0;
+            for (uint32_t pass = 0; pass < passes; ++pass) {
+                const uint32_t nf = (p->n_frames - done + (passes - pass) - 1) / (passes - pass);
+                KParams Q = P;
+                Q.first_frame = p->first_frame + done;
+                Q.n_frames = nf;
+                uint32_t n_chunks = std::min(want, nf);
+                const uint32_t F = (nf + n_chunks - 1) / n_chunks;
+                n_chunks = (nf + F - 1) / F;
+                Q.n_chunks = n_chunks; Q.chunk_frames = F; Q.items_per_chunk = (uint32_t)items_px;
+                if (items_px * n_chunks >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
+                Q.n_items = (uint32_t)(items_px * n_chunks);
+                if (n_chunks > 1) {
+                    const size_t plane = (size_t)px_local * (nf - F);
+                    if (3 * plane > c->lbuf_floats) {
+                        HIPC(c, hipStreamSynchronize(c->stream));
+                        dfree(c->d_lbuf);
+                        c->lbuf_floats = 0;
+                        HIPC(c, hipMalloc((void**)&c->d_lbuf, 3 * plane * sizeof(float)));
+                        c->lbuf_floats = 3 * plane;
+                    }
+                    Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local; Q.lbuf_plane = plane;
+                }
+                HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
+                HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
+                HIPC(c, rt_launch_finalize_chunks(Q, (uint32_t)px_local, c->stream));
+                c->stats.n_chunks = n_chunks;
+                done += nf;
+            }
+            c->stats.n_passes = passes;
         }
         c->stats.grid = grid;
         HIPC(c, hipEventRecord(c->ev1, c->stream));

@@ -25,6 +25,12 @@ struct KParams {
     // pixels of this device: row bands of `band` rows dealt round-robin over `nranks`
     uint32_t band, rank, nranks, n_local_rows;
     uint32_t tiles_x; uint32_t n_items;
+    // frame chunks: a pixel's n_frames are split into n_chunks work items of chunk_frames frames so
+    // that a frame-range tail does not serialize a launch with few pixels per lane (multi-GPU bands);
+    // chunk 0 accumulates into accum, later chunks store their samples (3 planes of floats,
+    // frame-major: [frame - chunk_frames][local]) for the in-order sum of finalize_chunks_kernel
+    uint32_t n_chunks, chunk_frames, items_per_chunk;
+    float* lbuf; size_t lbuf_stride, lbuf_plane;
     // outputs (compact local pixel order: local_row * W + x)
     float4* accum; uint32_t* rgba;
     // scratch
@@ -52,6 +58,7 @@ hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, u
 hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 hipError_t rt_launch_world_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* ent, int32_t* tri, float* tb,
                                  hipStream_t stream);
+hipError_t rt_launch_finalize_chunks(const KParams& P, uint32_t n_px, hipStream_t stream);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);
 

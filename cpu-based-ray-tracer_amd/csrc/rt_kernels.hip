@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     uint32_t w_rounds = 0, w_steps = 0, w_mt = 0, w_service = 0, w_fold = 0;
     bool alive = true, have_pixel = false, in_path = false;
     uint32_t local = 0, px = 0, x = 0, y = 0, k = 0;
+    uint32_t chunk = 0, kbase = 0, kend = 0;   // this item's frames: kbase + [0, kend) of the pixel
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     Rng g;
     Ray ray;
@@ -359,15 +360,28 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     P.gb_color[local] = make_float4(L.x, L.y, L.z, 0.0f);
                     have_pixel = false;
                 } else {
-                // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
-                acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
+                if (chunk == 0) {
+                    // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
+                    acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
+                } else {
+                    // a later chunk of the pixel's frames: the sample waits in the frame-major
+                    // buffer for the in-order sum of rt_finalize_chunks
+                    const size_t at = (size_t)(kbase + k - P.chunk_frames) * P.lbuf_stride + local;
+                    P.lbuf[at] = L.x;
+                    P.lbuf[at + P.lbuf_plane] = L.y;
+                    P.lbuf[at + 2 * P.lbuf_plane] = L.z;
+                }
                 ++k;
-                if (k == P.n_frames) {
-                    const float fr = (float)(P.first_frame + k - 1u);
-                    const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
-                    const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
-                    P.accum[local] = acc;
-                    P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+                if (k == kend) {
+                    if (chunk == 0) {
+                        P.accum[local] = acc;
+                        if (P.n_chunks == 1) {
+                            const float fr = (float)(P.first_frame + k - 1u);
+                            const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
+                            const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
+                            P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+                        }
+                    }
                     have_pixel = false;
                 }
                 }
@@ -393,8 +407,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 if (w >= P.n_items) {
                     alive = false;
                 } else {
-                    // 8x8 tile swizzle in local (row, column) space
-                    const uint32_t tile = w >> 6, within = w & 63u;
+                    // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
+                    const uint32_t c = w / P.items_per_chunk, wp = w - c * P.items_per_chunk;
+                    const uint32_t tile = wp >> 6, within = wp & 63u;
                     const uint32_t trow = tile / P.tiles_x, tcol = tile - trow * P.tiles_x;
                     const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
                     if (lr < P.n_local_rows && lx < P.W) {
@@ -406,7 +421,10 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         px = y * P.W + x;
                         have_pixel = true;
                         k = 0;
-                        if (!GB) acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
+                        chunk = c;
+                        kbase = c * P.chunk_frames;
+                        kend = min(P.chunk_frames, P.n_frames - kbase);
+                        if (!GB && c == 0) acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
                     }
                 }
             }
@@ -414,7 +432,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
 
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
-            g.start(P.seed, px, P.first_frame + k);
+            g.start(P.seed, px, P.first_frame + kbase + k);
             float cx, cy;
             if (GB) {   // centre of the pixel, DN/Camera.cpp:133
                 cx = ((float)x + 0.5f) / (float)P.W;
@@ -619,6 +637,36 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
         case 1: return occ_one<false, false, true>(block, lds_bytes);
         default: return occ_one<false, false, false>(block, 0);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// in-order completion of chunked pixels: accum (after chunk 0) += every later frame's sample in frame
+// order, then clamp + pack (MC/Renderer.cpp:128-133).  One thread per local pixel; the frame-major
+// buffer makes each frame's read coalesced across the pixels.
+__global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_t n_px)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_px) return;
+    float4 acc = P.accum[i];
+    for (uint32_t f = P.chunk_frames; f < P.n_frames; ++f) {
+        const size_t at = (size_t)(f - P.chunk_frames) * P.lbuf_stride + i;
+        acc.x = acc.x + P.lbuf[at];
+        acc.y = acc.y + P.lbuf[at + P.lbuf_plane];
+        acc.z = acc.z + P.lbuf[at + 2 * P.lbuf_plane];
+        acc.w = acc.w + 1.0f;
+    }
+    const float fr = (float)(P.first_frame + P.n_frames - 1u);
+    const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
+    const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
+    P.accum[i] = acc;
+    P.rgba[i] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+}
+
+hipError_t rt_launch_finalize_chunks(const KParams& P, uint32_t n_px, hipStream_t stream)
+{
+    if (n_px == 0 || P.n_chunks <= 1) return hipSuccess;
+    hipLaunchKernelGGL(finalize_chunks_kernel, dim3((n_px + 255) / 256), dim3(256), 0, stream, P, n_px);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -181,6 +181,9 @@ typedef struct {
      * work-queue + camera-ray, and traversal rounds; lanes served per service round (sum) */
     uint64_t wave_fold, cycles_service, cycles_queue, cycles_trace, service_lanes;
     float last_denoise_ms;    /* rt_render_denoised: the joint bilateral + temporal kernels (HIP events) */
+    uint32_t n_chunks;        /* frame chunks per pixel of the last rt_render's (last) launch: 1 unless the
+                                 launch has few pixels per lane; last_kernel_ms covers the in-order finalize */
+    uint32_t n_passes;        /* launches over consecutive frame ranges (bounded parked-sample memory) */
 } rt_stats;
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""A/B of context-level knobs read from the environment at rt_create (RT_THRESH, RT_STEPS, RT_VARIANT,
+RT_CHUNKS, RT_ITEMS_PER_LANE, RT_MIN_PX_PER_LANE) in ONE process, interleaved rounds, optionally on a
+row band of an N-rank frame (--rank/--nranks) to see multi-GPU per-rank behaviour on one GPU.
+
+    python tools/sweep_env.py --set "RT_CHUNKS=1" --set "RT_CHUNKS=2" --nranks 8
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+from _rt import rt  # noqa: E402
+
+KNOBS = ("RT_THRESH", "RT_STEPS", "RT_VARIANT", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--set", action="append", default=[], help="space/comma separated K=V assignments for one variant")
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--fast", action="store_true")
+    args = ap.parse_args()
+    W, H, spp = args.width, args.height, args.spp
+    scene = rt.Scene.cornell()
+    cam, _, _ = rt.camera_default(W, H)
+    variants = args.set or [""]
+    ctxs = []
+    for v in variants:
+        for k in KNOBS:
+            os.environ.pop(k, None)
+        for a in v.replace(",", " ").split():
+            k, val = a.split("=")
+            os.environ[k] = val
+        c = rt.Context(0)
+        c.upload(scene)
+        c.resize(W, H, 8, args.rank, args.nranks)
+        ctxs.append((v, c, []))
+    for r in range(args.rounds + 1):
+        for v, c, res in ctxs:
+            c.render(cam, spp, fetch=False, exact=not args.fast)
+            if r > 0:
+                res.append(c.stats().last_kernel_ms)
+    for v, c, res in ctxs:
+        ms = float(np.median(res))
+        print(json.dumps({"set": v, "rank": args.rank, "nranks": args.nranks, "kernel_ms": round(ms, 2), "n_chunks": c.stats().n_chunks,
+                          "msamples_per_s_rank": round(c.local_rows * W * spp / ms / 1e3, 1)}), flush=True)
+        c.close()
+
+
+if __name__ == "__main__":
+    main()
