@@ -14,6 +14,18 @@ Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlan
 {
 }
 
+Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 p, rt::vec3 f)
+    : position{p}, forward_direction{f}, vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance},
+      far_clip_plane_distance{FarClipPlaneDistance}
+{
+}
+
+void Camera::SetPosition(rt::vec3 p)
+{
+    position = p;
+    RecomputeViewMatrix();
+}
+
 void Camera::RecomputeProjectionMatrix()
 {   // MC/Camera.cpp:101-105
     const float p[3] = {position.x, position.y, position.z}, f[3] = {forward_direction.x, forward_direction.y, forward_direction.z};
@@ -240,3 +252,183 @@ float Renderer::LastKernelMilliseconds() const
     if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
     return st.last_kernel_ms;
 }
+
+// ============================================================================ WhittedRenderer
+#include "rt/WhittedRenderer.h"
+#include "rt/DenoisingRenderer.h"
+
+namespace rt {
+
+void WhittedRenderer::check(rt_status s, const char* what) const
+{
+    if (s != RT_OK) throw Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
+}
+
+WhittedRenderer::WhittedRenderer(rt_scene* built_scene, const Settings& s) : settings(s)
+{
+    rt_device_cfg cfg{settings.device, nullptr, 0};
+    check(rt_create(&ctx, &cfg), "rt_create");
+    check(rt_upload_scene(ctx, built_scene), "rt_upload_scene");
+}
+
+WhittedRenderer::~WhittedRenderer() { rt_destroy(ctx); }
+
+namespace {
+struct SceneGuard {
+    rt_scene* s = nullptr;
+    ~SceneGuard() { rt_scene_destroy(s); }
+};
+}  // namespace
+
+std::unique_ptr<WhittedRenderer> WhittedRenderer::TwoSpheres(const Settings& s)
+{   // Renderer::Renderer(), WH/Renderer.cpp:27-49
+    SceneGuard g;
+    if (rt_scene_create(&g.s) != RT_OK || rt_scene_add_two_spheres_scene(g.s) != RT_OK || rt_scene_build(g.s) != RT_OK)
+        throw Error("TwoSpheres: scene build failed");
+    return std::make_unique<WhittedRenderer>(g.s, s);
+}
+
+std::unique_ptr<WhittedRenderer> WhittedRenderer::BVHRayTracer(const std::string& bunny_obj, const std::string& teapot_obj, const Settings& s)
+{   // Renderer::Renderer(), BV/Renderer.cpp:26-43
+    SceneGuard g;
+    if (rt_scene_create(&g.s) != RT_OK) throw Error("BVHRayTracer: rt_scene_create failed");
+    if (rt_scene_add_bvh_tracer_scene(g.s, bunny_obj.c_str(), teapot_obj.c_str()) != RT_OK) throw Error("BVHRayTracer: cannot load the OBJ files");
+    if (rt_scene_build(g.s) != RT_OK) throw Error("BVHRayTracer: scene build failed");
+    return std::make_unique<WhittedRenderer>(g.s, s);
+}
+
+void WhittedRenderer::ResizeViewport(uint32_t width, uint32_t height)
+{   // BV/Renderer.cpp:45-67, WH/Renderer.cpp:51-80
+    if (frame_image_final) {
+        if (frame_image_final->GetWidth() == width && frame_image_final->GetHeight() == height) return;
+        frame_image_final->Resize(width, height);
+    } else {
+        frame_image_final = std::make_shared<Image>(width, height);
+    }
+    check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
+    frame_accumulating = 1;
+}
+
+void WhittedRenderer::Render(const Camera& camera) { RenderFrames(camera, 1); }
+
+void WhittedRenderer::RenderFrames(const Camera& camera, uint32_t n)
+{   // Render + RayGen_Shader: every frame is the same deterministic image, accumulated in order
+    if (!frame_image_final) throw Error("Render before ResizeViewport");
+    if (!settings.accumulating && n > 1) n = 1;
+    const rt_camera cam = camera.Native();
+    rt_render_params p{frame_accumulating, n, 0, 0.0f, RT_RENDER_WHITTED};
+    check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
+    if (settings.accumulating) frame_accumulating += n;
+    else frame_accumulating = 1;
+}
+
+float WhittedRenderer::LastKernelMilliseconds() const
+{
+    rt_stats st{};
+    if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
+    return st.last_kernel_ms;
+}
+
+// ============================================================================ DenoisingRenderer
+void DenoisingRenderer::check(rt_status s, const char* what) const
+{
+    if (s != RT_OK) throw Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
+}
+
+DenoisingRenderer::DenoisingRenderer() : DenoisingRenderer(Settings{}) {}
+
+DenoisingRenderer::DenoisingRenderer(const Settings& s) : settings(s)
+{
+    rt_denoise_params_default(&params);   // Denoising::Denoiser's member defaults (DN/Denoiser.h:333-358)
+    rt_device_cfg cfg{settings.device, nullptr, 0};
+    check(rt_create(&ctx, &cfg), "rt_create");
+    SceneGuard g;
+    check(rt_scene_create(&g.s), "rt_scene_create");
+    check(rt_scene_add_cornell_box(g.s), "rt_scene_add_cornell_box");   // DN/Renderer.cpp:26-58
+    check(rt_scene_build(g.s), "rt_scene_build");
+    check(rt_upload_scene(ctx, g.s), "rt_upload_scene");
+}
+
+DenoisingRenderer::~DenoisingRenderer() { rt_destroy(ctx); }
+
+void DenoisingRenderer::ResizeViewport(uint32_t width, uint32_t height)
+{   // DN/Renderer.cpp:60-99 (denoiser.Resize drops the history)
+    if (frame_image_final) {
+        if (frame_image_final->GetWidth() == width && frame_image_final->GetHeight() == height) return;
+        frame_image_final->Resize(width, height);
+    } else {
+        frame_image_final = std::make_shared<Image>(width, height);
+    }
+    check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
+    RestartTemporal();
+}
+
+void DenoisingRenderer::RestartTemporal() { check(rt_denoise_restart(ctx), "rt_denoise_restart"); }
+
+void DenoisingRenderer::resolve_settings()
+{   // Renderer::Render's settings -> denoiser members, DN/Renderer.cpp:108-241 (the members persist)
+    Settings& s = settings;   // (the reference's `settings.disable_JointBilateralFiltering == false;` lines have no effect)
+    if (s.disable_JointBilateralFiltering) {
+        jbf_on = false;
+        s.using_JointBilateralFiltering_15 = s.using_JointBilateralFiltering_33 = s.using_JointBilateralFiltering_65 = false;
+    } else if (s.using_JointBilateralFiltering_15) {
+        jbf_on = true; jbf_half = 3;
+        s.using_JointBilateralFiltering_33 = s.using_JointBilateralFiltering_65 = false;
+    } else if (s.using_JointBilateralFiltering_33) {
+        jbf_on = true; jbf_half = 16;
+        s.using_JointBilateralFiltering_15 = s.using_JointBilateralFiltering_65 = false;
+    } else if (s.using_JointBilateralFiltering_65) {
+        jbf_on = true; jbf_half = 32;
+        s.using_JointBilateralFiltering_15 = s.using_JointBilateralFiltering_33 = false;
+    }
+    if (s.disable_TemporalFiltering) {
+        temporal_on = false;
+        s.using_temporal_kernel_7 = s.using_temporal_kernel_15 = s.using_temporal_kernel_33 = false;
+        s.using_temporal_variance_tolerance_1 = s.using_temporal_variance_tolerance_2 = s.using_temporal_variance_tolerance_3 = false;
+        s.using_temporal_current_frame_weighting_10 = s.using_temporal_current_frame_weighting_5 = false;
+        s.using_temporal_current_frame_weighting_20 = false;
+    } else {
+        if (s.using_temporal_kernel_7) { temporal_on = true; temporal_half = 3; s.using_temporal_kernel_15 = s.using_temporal_kernel_33 = false; }
+        else if (s.using_temporal_kernel_15) { temporal_on = true; temporal_half = 7; s.using_temporal_kernel_7 = s.using_temporal_kernel_33 = false; }
+        else if (s.using_temporal_kernel_33) { temporal_on = true; temporal_half = 16; s.using_temporal_kernel_15 = s.using_temporal_kernel_7 = false; }
+        if (s.using_temporal_variance_tolerance_1) { temporal_on = true; params.tolerance = 1.0f; s.using_temporal_variance_tolerance_2 = s.using_temporal_variance_tolerance_3 = false; }
+        else if (s.using_temporal_variance_tolerance_2) { temporal_on = true; params.tolerance = 2.0f; s.using_temporal_variance_tolerance_1 = s.using_temporal_variance_tolerance_3 = false; }
+        else if (s.using_temporal_variance_tolerance_3) { temporal_on = true; params.tolerance = 3.0f; s.using_temporal_variance_tolerance_2 = s.using_temporal_variance_tolerance_1 = false; }
+        if (s.using_temporal_current_frame_weighting_5) {
+            temporal_on = true; params.current_frame_weighting = 0.05f;
+            s.using_temporal_current_frame_weighting_10 = s.using_temporal_current_frame_weighting_20 = s.using_temporal_current_frame_weighting_50 = false;
+        } else if (s.using_temporal_current_frame_weighting_10) {
+            temporal_on = true; params.current_frame_weighting = 0.1f;
+            s.using_temporal_current_frame_weighting_5 = s.using_temporal_current_frame_weighting_20 = s.using_temporal_current_frame_weighting_50 = false;
+        } else if (s.using_temporal_current_frame_weighting_20) {
+            temporal_on = true; params.current_frame_weighting = 0.2f;
+            s.using_temporal_current_frame_weighting_10 = s.using_temporal_current_frame_weighting_5 = s.using_temporal_current_frame_weighting_50 = false;
+        } else if (s.using_temporal_current_frame_weighting_50) {
+            temporal_on = true; params.current_frame_weighting = 0.5f;
+            s.using_temporal_current_frame_weighting_10 = s.using_temporal_current_frame_weighting_20 = s.using_temporal_current_frame_weighting_5 = false;
+        }
+    }
+    params.jbf_half_size = jbf_on ? jbf_half : 0;
+    params.temporal_half_size = temporal_on ? temporal_half : 0;
+    params.immediate_clamp = s.immediate_clamping ? 1 : 0;
+}
+
+void DenoisingRenderer::Render(const Camera& camera)
+{   // Renderer::Render, DN/Renderer.cpp:101-283
+    if (!frame_image_final) throw Error("Render before ResizeViewport");
+    resolve_settings();
+    ++frame;
+    const rt_camera cam = camera.Native();
+    check(rt_render_denoised(ctx, &cam, camera.ProjectionMatrix().data(), camera.ViewMatrix().data(), frame, settings.seed,
+                             RR_survival_probability, &params, frame_image_final->Data(), nullptr),
+          "rt_render_denoised");
+}
+
+float DenoisingRenderer::LastFrameMilliseconds() const
+{
+    rt_stats st{};
+    if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
+    return st.last_kernel_ms + st.last_denoise_ms;
+}
+
+}  // namespace rt

@@ -10,6 +10,14 @@
 //                          accumulation (offline prototype color.h:33-51)
 //
 //   rt_render_ppm W H SPP out.ppm [--seed S] [--rr P] [--fast] [--per-frame] [--offline G] [--obj FILE R G B]...
+//
+// The reference's other projects, through their drop-ins (include/rt/WhittedRenderer.h,
+// include/rt/DenoisingRenderer.h); SPP = frames:
+//   --project spheres                 Whitted Style Ray Tracer (two spheres, chessboard)
+//   --project bvh BUNNY.obj TEAPOT.obj  BVH Ray Tracer (bunny + teapot)
+//   --project denoiser [--jbf 15|33|65] [--temporal 7|15|33] [--tolerance 1|2|3] [--weighting 5|10|20|50]
+//             [--no-clamp] [--move-x D]   Denoiser (per frame: 1 spp + G-buffer + filters); --move-x
+//                                         moves the camera by D along x per frame (position = start + k*D)
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,7 +25,9 @@
 #include <string>
 #include <vector>
 
+#include "rt/DenoisingRenderer.h"
 #include "rt/Renderer.h"
+#include "rt/WhittedRenderer.h"
 
 namespace {
 
@@ -65,6 +75,81 @@ bool write_p3_offline(const char* path, const std::vector<float>& acc, uint32_t 
     return std::fclose(f) == 0;
 }
 
+// the BVH / Whitted / Denoiser projects (their mainloop.cpp's Render loop, headless)
+int run_project(int argc, char** argv, int i, uint32_t W, uint32_t H, uint32_t frames, const char* out, uint64_t seed)
+{
+    const std::string proj = argv[i];
+    try {
+        if (proj == "spheres" || proj == "bvh") {
+            std::unique_ptr<rt::WhittedRenderer> r;
+            Camera camera = proj == "spheres" ? rt::WhittedRenderer::TwoSpheresCamera() : rt::WhittedRenderer::BVHRayTracerCamera();
+            if (proj == "spheres") r = rt::WhittedRenderer::TwoSpheres();
+            else {
+                if (i + 2 >= argc) { std::fprintf(stderr, "--project bvh BUNNY.obj TEAPOT.obj\n"); return 2; }
+                r = rt::WhittedRenderer::BVHRayTracer(argv[i + 1], argv[i + 2]);
+            }
+            r->ResizeViewport(W, H);
+            camera.ResizeViewport(W, H);
+            for (uint32_t f = 0; f < frames; ++f) r->Render(camera);
+            if (!write_p6(out, *r->GetFinalImage())) { std::fprintf(stderr, "cannot write %s\n", out); return 1; }
+            std::printf("{\"project\": \"%s\", \"width\": %u, \"height\": %u, \"frames\": %u, \"kernel_ms\": %.3f}\n", proj.c_str(), W, H,
+                        r->GetSPP(), r->LastKernelMilliseconds());
+            return 0;
+        }
+        if (proj == "denoiser") {
+            rt::DenoisingRenderer::Settings st;
+            st.seed = seed;
+            float move_x = 0.0f;
+            for (int k = i + 1; k < argc; ++k) {
+                const std::string a = argv[k];
+                const int v = (k + 1 < argc) ? std::atoi(argv[k + 1]) : 0;
+                if (a == "--jbf") {
+                    st.disable_JointBilateralFiltering = false;
+                    st.using_JointBilateralFiltering_15 = v == 15; st.using_JointBilateralFiltering_33 = v == 33; st.using_JointBilateralFiltering_65 = v == 65;
+                    ++k;
+                } else if (a == "--temporal") {
+                    st.disable_TemporalFiltering = false;
+                    st.using_temporal_kernel_7 = v == 7; st.using_temporal_kernel_15 = v == 15; st.using_temporal_kernel_33 = v == 33;
+                    ++k;
+                } else if (a == "--tolerance") {
+                    st.using_temporal_variance_tolerance_1 = v == 1; st.using_temporal_variance_tolerance_2 = v == 2; st.using_temporal_variance_tolerance_3 = v == 3;
+                    ++k;
+                } else if (a == "--weighting") {
+                    st.using_temporal_current_frame_weighting_5 = v == 5; st.using_temporal_current_frame_weighting_10 = v == 10;
+                    st.using_temporal_current_frame_weighting_20 = v == 20; st.using_temporal_current_frame_weighting_50 = v == 50;
+                    ++k;
+                } else if (a == "--no-clamp") {
+                    st.immediate_clamping = false;
+                } else if (a == "--move-x" && k + 1 < argc) {
+                    move_x = std::strtof(argv[++k], nullptr);
+                } else {
+                    std::fprintf(stderr, "unknown denoiser argument %s\n", a.c_str());
+                    return 2;
+                }
+            }
+            rt::DenoisingRenderer r(st);
+            Camera camera(35.0f, 0.1f, 100.0f);   // DN/mainloop.cpp:22
+            const rt::vec3 p0 = camera.Position();
+            r.ResizeViewport(W, H);
+            camera.ResizeViewport(W, H);
+            for (uint32_t f = 0; f < frames; ++f) {
+                camera.SetPosition(rt::vec3{p0.x + move_x * (float)f, p0.y, p0.z});
+                r.Render(camera);
+            }
+            if (!write_p6(out, *r.GetFinalImage())) { std::fprintf(stderr, "cannot write %s\n", out); return 1; }
+            const rt_denoise_params dp = r.Resolved();
+            std::printf("{\"project\": \"denoiser\", \"width\": %u, \"height\": %u, \"frames\": %u, \"jbf_half\": %d, \"temporal_half\": %d, "
+                        "\"frame_ms\": %.3f}\n", W, H, frames, dp.jbf_half_size, dp.temporal_half_size, r.LastFrameMilliseconds());
+            return 0;
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 1;
+    }
+    std::fprintf(stderr, "unknown project %s\n", proj.c_str());
+    return 2;
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -83,6 +168,7 @@ int main(int argc, char** argv)
     std::vector<Obj> objs;
     for (int i = 5; i < argc; ++i) {
         const std::string a = argv[i];
+        if (a == "--project" && i + 1 < argc) return run_project(argc, argv, i + 1, W, H, spp, out, s.seed);
         if (a == "--seed" && i + 1 < argc) s.seed = std::strtoull(argv[++i], nullptr, 10);
         else if (a == "--rr" && i + 1 < argc) rr = std::strtof(argv[++i], nullptr);
         else if (a == "--fast") s.exact = false;

@@ -37,6 +37,12 @@ struct CameraInput {   // what Walnut::Input provided (MC/Camera.cpp:32-80)
 class Camera {
 public:
     Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance);
+    // the other projects' cameras differ only in their member defaults: the BVH Ray Tracer at
+    // (-1, 5, 10) and the Whitted Style Ray Tracer at (0, 0, 6), both looking down -z
+    // (BV/Camera.h:19-20, WH/Camera.h:17-19)
+    Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 position, rt::vec3 forward);
+    // what a UpdateCamera key press does to the position (e.g. a scripted camera path); recomputes the view
+    void SetPosition(rt::vec3 p);
 
     bool UpdateCamera(float dt);                                  // no input: recompute, never moves
     bool UpdateCamera(float dt, const rt::CameraInput& input);    // WASD/space/shift + mouse look

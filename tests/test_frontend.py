@@ -63,3 +63,43 @@ def test_frontend_offline_writer(tmp_path):
     v = 255 * np.clip(np.power(acc[..., :3].astype(np.float64) / 16, 0.5), 0, 1)
     want = np.where(v - np.floor(v) >= 0.5, np.floor(v) + 1, np.floor(v)).astype(np.int32)[::-1]
     assert np.array_equal(read_ppm(out), want)
+
+
+def rgb_of(rgba):
+    rgba = rgba.astype(np.uint32)
+    return np.stack([rgba & 0xFF, (rgba >> 8) & 0xFF, (rgba >> 16) & 0xFF], -1).astype(np.uint8)[::-1]
+
+
+@pytest.mark.gpu
+def test_frontend_whitted_spheres(tmp_path):
+    """rt::WhittedRenderer::TwoSpheres (the Whitted Style Ray Tracer's Renderer) through the front-end."""
+    out = tmp_path / "s.ppm"
+    subprocess.run([EXE, "160", "120", "3", str(out), "--project", "spheres"], check=True, capture_output=True)
+    z = np.load(os.path.join(O.GOLDEN, "c1_spheres.npz"))
+    assert np.array_equal(read_ppm(out), rgb_of(z["rgba_160x120_spp3"]))
+
+
+@pytest.mark.gpu
+def test_frontend_bvh_tracer(tmp_path):
+    """rt::WhittedRenderer::BVHRayTracer (the BVH Ray Tracer's Renderer) from OBJ files."""
+    from _rt import rt
+    b = np.load(os.path.join(O.GOLDEN, "bvh_scene.npz"))
+    rt.write_obj(str(tmp_path / "bunny.obj"), b["raw_bunny"])
+    rt.write_obj(str(tmp_path / "teapot.obj"), b["raw_teapot"])
+    out = tmp_path / "b.ppm"
+    subprocess.run([EXE, "160", "120", "3", str(out), "--project", "bvh", str(tmp_path / "bunny.obj"), str(tmp_path / "teapot.obj")],
+                   check=True, capture_output=True)
+    z = np.load(os.path.join(O.GOLDEN, "bvh_images.npz"))
+    assert np.array_equal(read_ppm(out), rgb_of(z["rgba_160x120_spp3"]))
+
+
+@pytest.mark.gpu
+def test_frontend_denoiser(tmp_path):
+    """rt::DenoisingRenderer with the UI's settings flags (temporal 15-px kernel, tolerance 2, weighting
+    0.1, the camera moving along x): the third frame equals the reference's."""
+    out = tmp_path / "d.ppm"
+    r = subprocess.run([EXE, "96", "72", "3", str(out), "--seed", "5", "--project", "denoiser", "--temporal", "15", "--tolerance", "2",
+                        "--weighting", "10", "--move-x", "0.08"], check=True, capture_output=True, text=True)
+    assert '"temporal_half": 7' in r.stdout and '"jbf_half": 0' in r.stdout
+    z = np.load(os.path.join(O.GOLDEN, "denoiser.npz"))
+    assert np.array_equal(read_ppm(out), rgb_of(z["temporal_f3_rgba"]))
