@@ -401,6 +401,10 @@ class Context:
         self._check(lib().rt_render(self.h, C.byref(cam), C.byref(p), None, None), "rt_render")
         return None
 
+    def reset_accumulation(self):
+        """Renderer::Reaccumulate (MC/Renderer.h:57-60): zero the accumulation buffer."""
+        self._check(lib().rt_reset_accumulation(self.h), "rt_reset_accumulation")
+
     def stats(self):
         s = Stats()
         self._check(lib().rt_get_stats(self.h, C.byref(s)), "rt_get_stats")

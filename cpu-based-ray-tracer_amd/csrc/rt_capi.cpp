@@ -64,6 +64,8 @@ struct rt_ctx {
     uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch (RT_LBUF_BUDGET_MB); C4 needs 20 GB of 288
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
+    int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
+    uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
 
@@ -311,6 +313,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     c->device = cfg ? cfg->device : 0;
     if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_VARIANT")) c->variant = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -464,6 +468,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
     P.thresh = c->thresh; P.steps = c->steps; P.variant = c->variant;
+    P.lds_pad = c->lds_pad;
     if (c->gb_next) {
         P.gb_color = c->d_gb_color; P.gb_pos = c->d_gb_pos; P.gb_nrm = c->d_gb_nrm; P.gb_prim = c->d_gb_prim; P.gb_clamp = c->gb_clamp;
     }
@@ -475,12 +480,13 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
     if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
-        const size_t used = lds ? lds_bytes : 0;
+        const size_t used = (lds ? lds_bytes : 0) + rt_lane_state_lds_bytes() + c->lds_pad;
         const int occ0 = rt_megakernel_occupancy(exact, count, lds, (int)c->block, used);
         for (uint32_t lv = 8; lv > 0; --lv)
             if (rt_megakernel_occupancy(exact, count, lds, (int)c->block, used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
-    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
+    if (exact && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
+    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes() + c->lds_pad;
     int bpc = rt_megakernel_occupancy(exact, count, lds, (int)c->block, shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;

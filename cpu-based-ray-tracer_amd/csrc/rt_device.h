@@ -67,9 +67,11 @@ struct Rng {
     uint32_t k0, k1, pixel, frame, dim;
     uint32_t blk;
     uint32_t b0, b1, b2, b3;
-    __device__ __forceinline__ void start(uint64_t seed, uint32_t px, uint32_t fr)
+    // the key is set once per kernel (uniform: it stays in scalar registers), the counter per sample
+    __device__ __forceinline__ void key(uint64_t seed) { k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); }
+    __device__ __forceinline__ void start(uint32_t px, uint32_t fr)
     {
-        k0 = (uint32_t)seed; k1 = (uint32_t)(seed >> 32); pixel = px; frame = fr; dim = 0; blk = 0xFFFFFFFFu;
+        pixel = px; frame = fr; dim = 0; blk = 0xFFFFFFFFu;
     }
     __device__ __forceinline__ float next()
     {

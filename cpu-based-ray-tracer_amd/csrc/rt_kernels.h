@@ -37,6 +37,7 @@ struct KParams {
     uint32_t* work_counter;
     float4* stack_ld; int32_t* stack_mat; uint32_t stack_depth; uint32_t total_threads;
     uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
+    uint32_t lds_pad;               // diagnostic: unused dynamic LDS bytes per workgroup (occupancy experiments)
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
@@ -50,6 +51,7 @@ struct KParams {
 size_t rt_scene_lds_bytes(const KParams& P);
 // bytes of LDS per 256-lane workgroup for `levels` EXACT stack levels (float4 + u8 material per lane)
 size_t rt_stack_lds_bytes(uint32_t levels);
+size_t rt_lane_state_lds_bytes();   // the megakernel's per-lane cold state (256 lanes)
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)

@@ -31,6 +31,18 @@ using namespace rtd;
 
 namespace {
 
+// per-lane cold state in LDS: word offsets of the fields, [field][lane] (pt_megakernel)
+enum : uint32_t {
+    LS_ACC = 0,                 // chunk 0's accumulator (float4)
+    LS_SN = 4,                  // shading normal across the shadow ray
+    LS_SC1 = 7, LS_SC2 = 8, LS_SD2 = 9,
+    LS_PEND = 10, LS_PCOS = 13, // EXACT: pending level (Ld, cos)
+    LS_THR = 10, LS_LSUM = 13,  // FAST: throughput, radiance
+    LS_MATS = 16,               // shading material (bits 0-7), pending level's material (bits 8-15)
+    LS_LOCAL = 17, LS_XY = 18, LS_KBASE = 19, LS_KEND = 20,   // the work item
+    LS_WORDS = 21
+};
+
 struct SceneView {
     const float4* nodes;
     const float4* tris;
@@ -172,6 +184,14 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     float4* lstack = lds_scene + P.lds_scene_quads;
     uint8_t* lmat = reinterpret_cast<uint8_t*>(lstack + (size_t)P.lds_levels * 256);
     const uint32_t tib = threadIdx.x;
+    // the lane's cold state -- read and written only by the service code, never inside traversal --
+    // lives in LDS ([field][lane] words after the fold stack), so the registers carry what the
+    // traversal loops need and the kernel fits 5 waves per SIMD
+    float* lstate = reinterpret_cast<float*>(lmat + (size_t)P.lds_levels * 256u);
+    auto lsf = [&](uint32_t f) -> float& { return lstate[f * 256u + tib]; };
+    auto lsu = [&](uint32_t f) -> uint32_t& { return reinterpret_cast<uint32_t*>(lstate)[f * 256u + tib]; };
+    auto ls3 = [&](uint32_t f) { return V3{lsf(f), lsf(f + 1), lsf(f + 2)}; };
+    auto st3 = [&](uint32_t f, V3 v) { lsf(f) = v.x; lsf(f + 1) = v.y; lsf(f + 2) = v.z; };
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
     const float rr = P.rr;
     const V3 cam{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
@@ -182,21 +202,17 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     // COUNT diagnostics: wave-level executions (counted by the first active lane)
     uint32_t w_rounds = 0, w_steps = 0, w_mt = 0, w_service = 0, w_fold = 0;
     bool alive = true, have_pixel = false, in_path = false;
-    uint32_t local = 0, px = 0, x = 0, y = 0, k = 0;
-    uint32_t chunk = 0, kbase = 0, kend = 0;   // this item's frames: kbase + [0, kend) of the pixel
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint32_t k = 0;   // frame of the current item (the item's frames are LS_KBASE + [0, LS_KEND))
     Rng g;
+    g.key(P.seed);
     Ray ray;
     uint32_t depth = 0;
     bool shadow = false;            // the lane's current ray is a shadow ray
     double slen = 0.0;              // length(q - p) of the shadow ray
-    // shading context carried across the shadow ray: face-forwarded normal, material, and the
-    // occlusion-independent factors of the direct term
-    V3 sn{0, 0, 0}; int smat = 0; float sc1 = 0.0f, sc2 = 0.0f, sd2 = 0.0f;
-    // EXACT: the level waiting to learn whether its indirect ray continues the path
-    V3 pend_ld{0, 0, 0}; float pend_cos = 0.0f; int pend_mat = 0;
-    // FAST: forward throughput and radiance
-    V3 thr{1.0f, 1.0f, 1.0f}, Lsum{0, 0, 0};
+    // in LDS: the shading context carried across the shadow ray (face-forwarded normal LS_SN, material
+    // in LS_MATS bits 0-7, the occlusion-independent factors LS_SC1/SC2/SD2 of the direct term); EXACT:
+    // the level waiting to learn whether its indirect ray continues the path (LS_PEND, LS_PCOS, material
+    // in LS_MATS bits 8-15); FAST: forward throughput LS_THR and radiance LS_LSUM
     // traversal state of the lane's current ray (persists across service rounds)
     const uint32_t NN = S.n_nodes;
     uint32_t ti = NN;                        // next node (NN: no ray / finished)
@@ -235,11 +251,12 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         const V3 loc = add(ray.o, smul((float)tbest, ray.d));
                         const V3 N{tq3.x, tq3.y, tq3.z};
                         const V3 nf = glm_normalize((dot(N, neg(ray.d)) < 0.0f) ? neg(N) : N);
+                        const uint32_t local = lsu(LS_LOCAL);
                         P.gb_prim[local] = f2i(tq1.w);
                         P.gb_pos[local] = make_float4(loc.x, loc.y, loc.z, 0.0f);
                         P.gb_nrm[local] = make_float4(nf.x, nf.y, nf.z, 0.0f);
                     } else {
-                        P.gb_prim[local] = -1;
+                        P.gb_prim[lsu(LS_LOCAL)] = -1;
                     }
                 }
                 if (depth == 0) {
@@ -253,13 +270,14 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     }
                 } else if (ttri < 0 || emissive) {
                     // the indirect ray missed or hit the light: radiance_indirect = 0 (MC/Renderer.cpp:202)
-                    L = EXACT ? pend_ld : Lsum;
+                    L = ls3(EXACT ? LS_PEND : LS_LSUM);
                     fold_top = (int)depth - 2;
                     finished = true;
                 } else if (EXACT) {
                     // the pending level recurses into this hit: push it as stack level depth-1
                     const uint32_t lvl = depth - 1;
-                    const float4 e = make_float4(pend_ld.x, pend_ld.y, pend_ld.z, pend_cos);
+                    const float4 e = make_float4(lsf(LS_PEND), lsf(LS_PEND + 1), lsf(LS_PEND + 2), lsf(LS_PCOS));
+                    const uint32_t pend_mat = lsu(LS_MATS) >> 8;
                     if (lvl < P.lds_levels) {
                         lstack[lvl * 256u + tib] = e;
                         lmat[lvl * 256u + tib] = (uint8_t)pend_mat;
@@ -279,16 +297,17 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     const V3 N{tq3.x, tq3.y, tq3.z};
                     const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
                     const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
-                    sn = n; smat = mat;
+                    st3(LS_SN, n);
+                    lsu(LS_MATS) = (lsu(LS_MATS) & 0xFF00u) | (uint32_t)mat;
                     if (P.has_light) {
                         V3 q, nl0;
                         sample_light(S, P.light_area, g, q, nl0);
                         const V3 p2q = sub(q, p);
                         const V3 wl = glm_normalize(p2q);
                         const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
-                        sc1 = dot(wl, n);
-                        sc2 = dot(neg(wl), nl);
-                        sd2 = dot(p2q, p2q);
+                        lsf(LS_SC1) = dot(wl, n);
+                        lsf(LS_SC2) = dot(neg(wl), nl);
+                        lsf(LS_SD2) = dot(p2q, p2q);
                         slen = (double)glm_length(p2q);
                         ray = make_ray(p, wl);
                         shadow = true;
@@ -301,9 +320,10 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             } else {
                 // ------------ the shadow ray came back: direct term (MC/Renderer.cpp:187-189)
                 if (!toccl) {
-                    const float4 mb = S.mats[2 * smat];
+                    const float sc1 = lsf(LS_SC1);
+                    const float4 mb = S.mats[2 * (lsu(LS_MATS) & 0xFFu)];
                     const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};   // BRDF, MC/WhittedMaterial.h:58-69
-                    ld = divs(divs(muls(muls(mul(E, f), sc1), sc2), sd2), lpdf);
+                    ld = divs(divs(muls(muls(mul(E, f), sc1), lsf(LS_SC2)), lsf(LS_SD2)), lpdf);
                 }
                 shadow = false;
                 part2 = true;
@@ -313,22 +333,25 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 // ------------ shading, second half: Russian roulette + indirect direction
                 // (MC/Renderer.cpp:193-209; the depth cap only bounds the loop: P(depth > 4096) = rr^4096)
                 if (g.next() < rr && depth < 4096u) {
+                    const V3 sn = ls3(LS_SN);
+                    const uint32_t smat = lsu(LS_MATS) & 0xFFu;
                     const V3 wi = glm_normalize(sample_hemisphere(sn, g));
                     const float c = dot(wi, sn);
                     if (EXACT) {
-                        pend_ld = ld; pend_cos = c; pend_mat = smat;
+                        st3(LS_PEND, ld); lsf(LS_PCOS) = c; lsu(LS_MATS) = smat | (smat << 8);
                     } else {
-                        Lsum = add(Lsum, mul(thr, ld));
+                        const V3 thr = ls3(LS_THR);
+                        st3(LS_LSUM, add(ls3(LS_LSUM), mul(thr, ld)));
                         const float4 mb = S.mats[2 * smat];
                         const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        thr = muls(mul(thr, f), c / PDF / rr);
+                        st3(LS_THR, muls(mul(thr, f), c / PDF / rr));
                     }
                     ray = make_ray(ray.o, wi);
                     depth = depth + 1;
                     new_ray = true;
                 } else {
                     if (EXACT) L = ld;
-                    else { Lsum = add(Lsum, mul(thr, ld)); L = Lsum; }
+                    else L = add(ls3(LS_LSUM), mul(ls3(LS_THR), ld));
                     fold_top = (int)depth - 1;
                     finished = true;
                 }
@@ -357,12 +380,14 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 if (GB) {
                     // RayGen_Shader, DN/Renderer.cpp:264-275: (clamped) color into the G-buffer
                     if (P.gb_clamp) L = V3{smin(smax(L.x, 0.0f), 1.0f), smin(smax(L.y, 0.0f), 1.0f), smin(smax(L.z, 0.0f), 1.0f)};
-                    P.gb_color[local] = make_float4(L.x, L.y, L.z, 0.0f);
+                    P.gb_color[lsu(LS_LOCAL)] = make_float4(L.x, L.y, L.z, 0.0f);
                     have_pixel = false;
                 } else {
-                if (chunk == 0) {
-                    // temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
-                    acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
+                const uint32_t local = lsu(LS_LOCAL), kbase = lsu(LS_KBASE);
+                if (kbase == 0) {
+                    // chunk 0: temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
+                    lsf(LS_ACC) = lsf(LS_ACC) + L.x; lsf(LS_ACC + 1) = lsf(LS_ACC + 1) + L.y;
+                    lsf(LS_ACC + 2) = lsf(LS_ACC + 2) + L.z; lsf(LS_ACC + 3) = lsf(LS_ACC + 3) + 1.0f;
                 } else {
                     // a later chunk of the pixel's frames: the sample waits in the frame-major
                     // buffer for the in-order sum of rt_finalize_chunks
@@ -372,8 +397,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     P.lbuf[at + 2 * P.lbuf_plane] = L.z;
                 }
                 ++k;
-                if (k == kend) {
-                    if (chunk == 0) {
+                if (k == lsu(LS_KEND)) {
+                    if (kbase == 0) {
+                        const float4 acc = make_float4(lsf(LS_ACC), lsf(LS_ACC + 1), lsf(LS_ACC + 2), lsf(LS_ACC + 3));
                         P.accum[local] = acc;
                         if (P.n_chunks == 1) {
                             const float fr = (float)(P.first_frame + k - 1u);
@@ -415,16 +441,19 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     if (lr < P.n_local_rows && lx < P.W) {
                         // local row -> global row (row bands dealt round-robin over ranks)
                         const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
-                        y = (P.rank + band_k * P.nranks) * P.band + in_band;
-                        x = lx;
-                        local = lr * P.W + lx;
-                        px = y * P.W + x;
+                        const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
+                        const uint32_t local = lr * P.W + lx;
+                        const uint32_t kbase = c * P.chunk_frames;
+                        lsu(LS_LOCAL) = local;
+                        lsu(LS_XY) = lx | (y << 16);
+                        lsu(LS_KBASE) = kbase;
+                        lsu(LS_KEND) = min(P.chunk_frames, P.n_frames - kbase);
                         have_pixel = true;
                         k = 0;
-                        chunk = c;
-                        kbase = c * P.chunk_frames;
-                        kend = min(P.chunk_frames, P.n_frames - kbase);
-                        if (!GB && c == 0) acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
+                        if (!GB && c == 0) {
+                            const float4 a = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
+                            lsf(LS_ACC) = a.x; lsf(LS_ACC + 1) = a.y; lsf(LS_ACC + 2) = a.z; lsf(LS_ACC + 3) = a.w;
+                        }
                     }
                 }
             }
@@ -432,7 +461,8 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
 
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
-            g.start(P.seed, px, P.first_frame + kbase + k);
+            const uint32_t xy = lsu(LS_XY), x = xy & 0xFFFFu, y = xy >> 16;
+            g.start(y * P.W + x, P.first_frame + lsu(LS_KBASE) + k);
             float cx, cy;
             if (GB) {   // centre of the pixel, DN/Camera.cpp:133
                 cx = ((float)x + 0.5f) / (float)P.W;
@@ -454,7 +484,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             depth = 0;
             shadow = false;
             in_path = true;
-            if (!EXACT) { thr = V3{1.0f, 1.0f, 1.0f}; Lsum = V3{0, 0, 0}; }
+            if (!EXACT) { st3(LS_THR, V3{1.0f, 1.0f, 1.0f}); st3(LS_LSUM, V3{0, 0, 0}); }
             if (COUNT) ++rays;
             ti = 0; tbest = 1.7976931348623157e308; ttri = -1; toccl = false; tdone = false;
         }
@@ -598,6 +628,8 @@ int occ_one(int block, size_t lds)
 
 size_t rt_stack_lds_bytes(uint32_t levels) { return (size_t)levels * 256 * (sizeof(float4) + 1); }
 
+size_t rt_lane_state_lds_bytes() { return (size_t)LS_WORDS * 256 * sizeof(float); }
+
 size_t rt_scene_lds_bytes(const KParams& P)
 {
     return (size_t)(2 * P.n_nodes + 4 * P.n_tris + 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris) * sizeof(float4);
@@ -605,7 +637,7 @@ size_t rt_scene_lds_bytes(const KParams& P)
 
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream)
 {
-    const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0);
+    const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes() + P.lds_pad;
     if (P.gb_color) {   // the Denoiser's G-buffer frame (EXACT, no counters)
         if (lds) hipLaunchKernelGGL((pt_megakernel<true, false, true, true>), dim3(grid), dim3(block), sh, stream, P);
         else hipLaunchKernelGGL((pt_megakernel<true, false, false, true>), dim3(grid), dim3(block), sh, stream, P);
@@ -629,13 +661,13 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
     const int sel = (exact ? 4 : 0) | (count ? 2 : 0) | (lds ? 1 : 0);
     switch (sel) {
         case 7: return occ_one<true, true, true>(block, lds_bytes);
-        case 6: return occ_one<true, true, false>(block, 0);
+        case 6: return occ_one<true, true, false>(block, lds_bytes);
         case 5: return occ_one<true, false, true>(block, lds_bytes);
-        case 4: return occ_one<true, false, false>(block, 0);
+        case 4: return occ_one<true, false, false>(block, lds_bytes);
         case 3: return occ_one<false, true, true>(block, lds_bytes);
-        case 2: return occ_one<false, true, false>(block, 0);
+        case 2: return occ_one<false, true, false>(block, lds_bytes);
         case 1: return occ_one<false, false, true>(block, lds_bytes);
-        default: return occ_one<false, false, false>(block, 0);
+        default: return occ_one<false, false, false>(block, lds_bytes);
     }
 }
 

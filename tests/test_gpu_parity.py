@@ -198,3 +198,18 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
     finally:
         c.close()
     assert np.array_equal(bits(a), bits(b))
+
+
+@pytest.mark.parametrize("W,H,first,n", [(784, 784, 1, 4),        # C2 at full size
+                                         (1920, 1080, 1, 2),      # C4 at full size
+                                         (1920, 1080, 1021, 4)])  # C4's last frames (RNG counter, divisor)
+def test_full_size_matches_oracle(ctx, W, H, first, n):
+    """SURVEY.md §8(d) parity gate (ii): the configuration's full resolution against the CPU restatement,
+    at a few frames (the oracle runs multithreaded on the host).  Bitwise accumulation and RGBA8."""
+    ctx.resize(W, H)
+    ctx.reset_accumulation()
+    cam, _, _ = rt.camera_default(W, H)
+    rgba, acc = ctx.render(cam, n, first_frame=first, seed=0)
+    oacc, orgba, _ = O.Scene().render(W, H, n, seed=0, first_frame=first, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(bits(acc), bits(oacc))
+    assert np.array_equal(rgba, orgba)
