@@ -57,10 +57,10 @@ struct rt_ctx {
     hipEvent_t ev2 = nullptr, ev3 = nullptr;
     bool pending_denoise = false;
     bool gb_next = false, gb_clamp = true;   // rt_render_denoised -> rt_render: G-buffer mode
-    uint32_t variant = 0;
     // frame chunking (KParams::n_chunks): split when a launch has fewer than min_px_per_lane pixels
-    // per lane, into about items_per_lane items per lane (RT_CHUNKS forces a count)
-    uint32_t force_chunks = 0, items_per_lane = 32, min_px_per_lane = 32;
+    // per lane, into about items_per_lane items per lane but no chunk shorter than min_chunk_frames
+    // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
+    uint32_t force_chunks = 0, items_per_lane = 48, min_px_per_lane = 32, min_chunk_frames = 32;
     uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch (RT_LBUF_BUDGET_MB); C4 needs 20 GB of 288
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
@@ -315,10 +315,10 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_VARIANT")) c->variant = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_MIN_CHUNK_FRAMES")) c->min_chunk_frames = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
@@ -467,7 +467,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
-    P.thresh = c->thresh; P.steps = c->steps; P.variant = c->variant;
+    P.thresh = c->thresh; P.steps = c->steps;
     P.lds_pad = c->lds_pad;
     if (c->gb_next) {
         P.gb_color = c->d_gb_color; P.gb_pos = c->d_gb_pos; P.gb_nrm = c->d_gb_nrm; P.gb_prim = c->d_gb_prim; P.gb_clamp = c->gb_clamp;
@@ -480,13 +480,13 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
     if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
-        const size_t used = (lds ? lds_bytes : 0) + rt_lane_state_lds_bytes() + c->lds_pad;
+        const size_t used = (lds ? lds_bytes : 0) + rt_lane_state_lds_bytes(exact) + c->lds_pad;
         const int occ0 = rt_megakernel_occupancy(exact, count, lds, (int)c->block, used);
         for (uint32_t lv = 8; lv > 0; --lv)
             if (rt_megakernel_occupancy(exact, count, lds, (int)c->block, used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     if (exact && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
-    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes() + c->lds_pad;
+    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes(exact) + c->lds_pad;
     int bpc = rt_megakernel_occupancy(exact, count, lds, (int)c->block, shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
@@ -514,7 +514,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             if (!c->gb_next && p->n_frames > 1 && px_local > 0) {
                 if (c->force_chunks) want = std::min(c->force_chunks, p->n_frames);
                 else if (px_local < (uint64_t)c->min_px_per_lane * lanes)
-                    want = (uint32_t)std::min<uint64_t>(p->n_frames, ((uint64_t)c->items_per_lane * lanes + px_local - 1) / px_local);
+                    want = (uint32_t)std::min<uint64_t>({(uint64_t)p->n_frames, std::max<uint64_t>(1, p->n_frames / c->min_chunk_frames),
+                                                         ((uint64_t)c->items_per_lane * lanes + px_local - 1) / px_local});
             }
             uint32_t passes = 1;
             if (want > 1) {
@@ -534,7 +535,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 if (items_px * n_chunks >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
                 Q.n_items = (uint32_t)(items_px * n_chunks);
                 if (n_chunks > 1) {
-                    const size_t plane = (size_t)px_local * (nf - F);
+                    // 4-frame blocks of 12 floats per pixel (rt_kernels.hip)
+                    const size_t plane = (size_t)px_local * (((nf - F) + 3u) & ~3u);
                     if (3 * plane > c->lbuf_floats) {
                         HIPC(c, hipStreamSynchronize(c->stream));
                         dfree(c->d_lbuf);
@@ -542,7 +544,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                         HIPC(c, hipMalloc((void**)&c->d_lbuf, 3 * plane * sizeof(float)));
                         c->lbuf_floats = 3 * plane;
                     }
-                    Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local; Q.lbuf_plane = plane;
+                    Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local;
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
                 HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));

@@ -30,7 +30,7 @@ struct KParams {
     // chunk 0 accumulates into accum, later chunks store their samples (3 planes of floats,
     // frame-major: [frame - chunk_frames][local]) for the in-order sum of finalize_chunks_kernel
     uint32_t n_chunks, chunk_frames, items_per_chunk;
-    float* lbuf; size_t lbuf_stride, lbuf_plane;
+    float* lbuf; size_t lbuf_stride;
     // outputs (compact local pixel order: local_row * W + x)
     float4* accum; uint32_t* rgba;
     // scratch
@@ -42,7 +42,6 @@ struct KParams {
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
-    uint32_t variant;               // A/B of traversal-loop forms (RT_VARIANT; 0 = default)
     // the Denoiser's G-buffer frame (set => pt_megakernel<..., GB = true>); one sample per pixel
     float4* gb_color; float4* gb_pos; float4* gb_nrm; int32_t* gb_prim; uint32_t gb_clamp;
 };
@@ -51,7 +50,7 @@ struct KParams {
 size_t rt_scene_lds_bytes(const KParams& P);
 // bytes of LDS per 256-lane workgroup for `levels` EXACT stack levels (float4 + u8 material per lane)
 size_t rt_stack_lds_bytes(uint32_t levels);
-size_t rt_lane_state_lds_bytes();   // the megakernel's per-lane cold state (256 lanes)
+size_t rt_lane_state_lds_bytes(bool exact);   // the megakernel's per-lane cold state (256 lanes)
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)

@@ -33,15 +33,47 @@ namespace {
 
 // per-lane cold state in LDS: word offsets of the fields, [field][lane] (pt_megakernel)
 enum : uint32_t {
-    LS_ACC = 0,                 // chunk 0's accumulator (float4)
-    LS_SN = 4,                  // shading normal across the shadow ray
-    LS_SC1 = 7, LS_SC2 = 8, LS_SD2 = 9,
-    LS_PEND = 10, LS_PCOS = 13, // EXACT: pending level (Ld, cos)
-    LS_THR = 10, LS_LSUM = 13,  // FAST: throughput, radiance
-    LS_MATS = 16,               // shading material (bits 0-7), pending level's material (bits 8-15)
-    LS_LOCAL = 17, LS_XY = 18, LS_KBASE = 19, LS_KEND = 20,   // the work item
-    LS_WORDS = 21
+    LS_SN = 0,                  // shading normal across the shadow ray
+    LS_SC1 = 3, LS_SC2 = 4, LS_SD2 = 5,
+    LS_MATS = 6,                // shading material (bits 0-7), pending level's material (bits 8-15)
+    LS_LOCAL = 7, LS_XY = 8, LS_C = 9,   // the work item: local pixel, (x, y) global, frame chunk
+    LS_RNG = 10,                // the Philox block of the current 4 draws (4 words)
+    LS_PEND = 14, LS_PCOS = 17, // EXACT: pending level (Ld, cos)
+    LS_THR = 14, LS_LSUM = 17,  // FAST: throughput, radiance
+    LS_WORDS_EXACT = 18, LS_WORDS_FAST = 20
 };
+
+// Uniform draws of the lane's current sample: Walnut::Random::Float's formula (WN/Random.h:27-30) on
+// the Philox stream of (pixel, frame) (rt_device.h), the block of 4 draws buffered in LDS
+struct LaneRng {
+    uint32_t* buf;              // the lane's LS_RNG words (stride 256)
+    uint32_t k0, k1;            // key (uniform)
+    uint32_t pixel, frame, dim, blk;
+    __device__ __forceinline__ void start(uint32_t px, uint32_t fr) { pixel = px; frame = fr; dim = 0; blk = 0xFFFFFFFFu; }
+    __device__ __forceinline__ float next()
+    {
+        const uint32_t want = dim >> 2;
+        if (want != blk) {
+            uint32_t o[4];
+            philox4x32_10(pixel, frame, want, 0u, k0, k1, o);
+            buf[0] = o[0]; buf[256] = o[1]; buf[512] = o[2]; buf[768] = o[3];
+            blk = want;
+        }
+        const uint32_t u = buf[(dim & 3u) * 256u];
+        ++dim;
+        return (float)u / 4294967296.0f;   // (float)UINT32_MAX == 2^32 exactly
+    }
+};
+
+// The kernel's parameters re-read from the kernarg segment where a section uses them: the empty asm
+// keeps the compiler from hoisting the scalar loads to the kernel entry, where ~100 long-lived uniforms
+// overflow the SGPRs into VGPR lanes and cost the kernel a wave per SIMD.
+__device__ __forceinline__ const KParams& kargs()
+{
+    const KParams* kp = (const KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *kp;
+}
 
 struct SceneView {
     const float4* nodes;
@@ -106,7 +138,8 @@ __device__ __forceinline__ void traverse(const SceneView& S, const Ray& r, bool 
 
 // SamplingAreaLight -> TriangleMesh::Sampling -> BVH::Sampling_from_root/_node -> TrianglePrimitive::Sampling
 // (MC/Renderer.h:163-180, MC/TriangleMesh.h:193-197, MC/BVH.h:103-129, MC/TriangleMesh.h:69-89)
-__device__ __forceinline__ void sample_light(const SceneView& S, float light_area, Rng& g, V3& q, V3& nl)
+template <class G>
+__device__ __forceinline__ void sample_light(const SceneView& S, float light_area, G& g, V3& q, V3& nl)
 {
     const float u0 = g.next();
     float p = u0 * light_area;
@@ -129,7 +162,8 @@ __device__ __forceinline__ void sample_light(const SceneView& S, float light_are
 }
 
 // WhittedMaterial::Sampling, MC/WhittedMaterial.h:71-117
-__device__ __forceinline__ V3 sample_hemisphere(V3 n, Rng& g)
+template <class G>
+__device__ __forceinline__ V3 sample_hemisphere(V3 n, G& g)
 {
     const float z = g.next();
     const float rxy = __builtin_sqrtf(1.0f - z * z);
@@ -193,18 +227,15 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     auto ls3 = [&](uint32_t f) { return V3{lsf(f), lsf(f + 1), lsf(f + 2)}; };
     auto st3 = [&](uint32_t f, V3 v) { lsf(f) = v.x; lsf(f + 1) = v.y; lsf(f + 2) = v.z; };
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
-    const float rr = P.rr;
-    const V3 cam{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
-    const V3 E{P.light_emission[0], P.light_emission[1], P.light_emission[2]};
-    const float lpdf = 1.0f / P.light_area;   // BVH::Sampling_from_root overwrites PDF (MC/BVH.h:106)
 
     uint32_t node_tests = 0, tri_tests = 0, rays = 0;
     // COUNT diagnostics: wave-level executions (counted by the first active lane)
     uint32_t w_rounds = 0, w_steps = 0, w_mt = 0, w_service = 0, w_fold = 0;
     bool alive = true, have_pixel = false, in_path = false;
-    uint32_t k = 0;   // frame of the current item (the item's frames are LS_KBASE + [0, LS_KEND))
-    Rng g;
-    g.key(P.seed);
+    uint32_t k = 0;   // frame of the current item (item of chunk c: frames c * chunk_frames + [0, kend))
+    LaneRng g;
+    g.buf = reinterpret_cast<uint32_t*>(lstate) + LS_RNG * 256u + tib;
+    g.k0 = (uint32_t)P.seed; g.k1 = (uint32_t)(P.seed >> 32);
     Ray ray;
     uint32_t depth = 0;
     bool shadow = false;            // the lane's current ray is a shadow ray
@@ -231,6 +262,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             s_lanes += (uint64_t)__popcll(__ballot(in_path && tdone));
         }
         if (in_path && tdone) {
+            const KParams& Q = kargs();
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
             V3 L{0, 0, 0};
@@ -252,11 +284,11 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         const V3 N{tq3.x, tq3.y, tq3.z};
                         const V3 nf = glm_normalize((dot(N, neg(ray.d)) < 0.0f) ? neg(N) : N);
                         const uint32_t local = lsu(LS_LOCAL);
-                        P.gb_prim[local] = f2i(tq1.w);
-                        P.gb_pos[local] = make_float4(loc.x, loc.y, loc.z, 0.0f);
-                        P.gb_nrm[local] = make_float4(nf.x, nf.y, nf.z, 0.0f);
+                        Q.gb_prim[local] = f2i(tq1.w);
+                        Q.gb_pos[local] = make_float4(loc.x, loc.y, loc.z, 0.0f);
+                        Q.gb_nrm[local] = make_float4(nf.x, nf.y, nf.z, 0.0f);
                     } else {
-                        P.gb_prim[lsu(LS_LOCAL)] = -1;
+                        Q.gb_prim[lsu(LS_LOCAL)] = -1;
                     }
                 }
                 if (depth == 0) {
@@ -278,14 +310,14 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     const uint32_t lvl = depth - 1;
                     const float4 e = make_float4(lsf(LS_PEND), lsf(LS_PEND + 1), lsf(LS_PEND + 2), lsf(LS_PCOS));
                     const uint32_t pend_mat = lsu(LS_MATS) >> 8;
-                    if (lvl < P.lds_levels) {
+                    if (lvl < Q.lds_levels) {
                         lstack[lvl * 256u + tib] = e;
                         lmat[lvl * 256u + tib] = (uint8_t)pend_mat;
-                    } else if (lvl < P.stack_depth) {
-                        P.stack_ld[(size_t)lvl * P.total_threads + gtid] = e;
-                        P.stack_mat[(size_t)lvl * P.total_threads + gtid] = pend_mat;
+                    } else if (lvl < Q.stack_depth) {
+                        Q.stack_ld[(size_t)lvl * Q.total_threads + gtid] = e;
+                        Q.stack_mat[(size_t)lvl * Q.total_threads + gtid] = pend_mat;
                     } else {
-                        atomicAdd((unsigned long long*)&P.counters[3], 1ull);   // reported as stack overflow
+                        atomicAdd((unsigned long long*)&Q.counters[3], 1ull);   // reported as stack overflow
                     }
                 }
                 if (!finished) {
@@ -299,9 +331,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
                     st3(LS_SN, n);
                     lsu(LS_MATS) = (lsu(LS_MATS) & 0xFF00u) | (uint32_t)mat;
-                    if (P.has_light) {
+                    if (Q.has_light) {
                         V3 q, nl0;
-                        sample_light(S, P.light_area, g, q, nl0);
+                        sample_light(S, Q.light_area, g, q, nl0);
                         const V3 p2q = sub(q, p);
                         const V3 wl = glm_normalize(p2q);
                         const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
@@ -323,7 +355,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     const float sc1 = lsf(LS_SC1);
                     const float4 mb = S.mats[2 * (lsu(LS_MATS) & 0xFFu)];
                     const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};   // BRDF, MC/WhittedMaterial.h:58-69
-                    ld = divs(divs(muls(muls(mul(E, f), sc1), lsf(LS_SC2)), lsf(LS_SD2)), lpdf);
+                    ld = divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), lsf(LS_SC2)), lsf(LS_SD2)), (1.0f / Q.light_area));
                 }
                 shadow = false;
                 part2 = true;
@@ -332,7 +364,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             if (part2) {
                 // ------------ shading, second half: Russian roulette + indirect direction
                 // (MC/Renderer.cpp:193-209; the depth cap only bounds the loop: P(depth > 4096) = rr^4096)
-                if (g.next() < rr && depth < 4096u) {
+                if (g.next() < Q.rr && depth < 4096u) {
                     const V3 sn = ls3(LS_SN);
                     const uint32_t smat = lsu(LS_MATS) & 0xFFu;
                     const V3 wi = glm_normalize(sample_hemisphere(sn, g));
@@ -344,7 +376,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         st3(LS_LSUM, add(ls3(LS_LSUM), mul(thr, ld)));
                         const float4 mb = S.mats[2 * smat];
                         const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        st3(LS_THR, muls(mul(thr, f), c / PDF / rr));
+                        st3(LS_THR, muls(mul(thr, f), c / PDF / Q.rr));
                     }
                     ray = make_ray(ray.o, wi);
                     depth = depth + 1;
@@ -364,48 +396,53 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_fold;
                         float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
                         int m = 0;
-                        if ((uint32_t)lvl < P.lds_levels) {
+                        if ((uint32_t)lvl < Q.lds_levels) {
                             e = lstack[(uint32_t)lvl * 256u + tib];
                             m = lmat[(uint32_t)lvl * 256u + tib];
-                        } else if ((uint32_t)lvl < P.stack_depth) {
-                            e = P.stack_ld[(size_t)lvl * P.total_threads + gtid];
-                            m = P.stack_mat[(size_t)lvl * P.total_threads + gtid];
+                        } else if ((uint32_t)lvl < Q.stack_depth) {
+                            e = Q.stack_ld[(size_t)lvl * Q.total_threads + gtid];
+                            m = Q.stack_mat[(size_t)lvl * Q.total_threads + gtid];
                         }
                         const float4 mb2 = S.mats[2 * m];
                         const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                        L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), rr));
+                        L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), Q.rr));
                     }
                 }
                 in_path = false;
                 if (GB) {
                     // RayGen_Shader, DN/Renderer.cpp:264-275: (clamped) color into the G-buffer
-                    if (P.gb_clamp) L = V3{smin(smax(L.x, 0.0f), 1.0f), smin(smax(L.y, 0.0f), 1.0f), smin(smax(L.z, 0.0f), 1.0f)};
-                    P.gb_color[lsu(LS_LOCAL)] = make_float4(L.x, L.y, L.z, 0.0f);
+                    if (Q.gb_clamp) L = V3{smin(smax(L.x, 0.0f), 1.0f), smin(smax(L.y, 0.0f), 1.0f), smin(smax(L.z, 0.0f), 1.0f)};
+                    Q.gb_color[lsu(LS_LOCAL)] = make_float4(L.x, L.y, L.z, 0.0f);
                     have_pixel = false;
                 } else {
-                const uint32_t local = lsu(LS_LOCAL), kbase = lsu(LS_KBASE);
+                const uint32_t local = lsu(LS_LOCAL), kbase = lsu(LS_C) * Q.chunk_frames;
+                float4 acc;
                 if (kbase == 0) {
-                    // chunk 0: temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133)
-                    lsf(LS_ACC) = lsf(LS_ACC) + L.x; lsf(LS_ACC + 1) = lsf(LS_ACC + 1) + L.y;
-                    lsf(LS_ACC + 2) = lsf(LS_ACC + 2) + L.z; lsf(LS_ACC + 3) = lsf(LS_ACC + 3) + 1.0f;
+                    // chunk 0: temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133), the
+                    // accumulator read-modified-written in place (L2-resident: the lane's own pixel)
+                    acc = Q.accum[local];
+                    acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
+                    Q.accum[local] = acc;
                 } else {
                     // a later chunk of the pixel's frames: the sample waits in the frame-major
                     // buffer for the in-order sum of rt_finalize_chunks
-                    const size_t at = (size_t)(kbase + k - P.chunk_frames) * P.lbuf_stride + local;
-                    P.lbuf[at] = L.x;
-                    P.lbuf[at + P.lbuf_plane] = L.y;
-                    P.lbuf[at + 2 * P.lbuf_plane] = L.z;
+                    const uint32_t fp = kbase + k - Q.chunk_frames;
+                    // 4-frame blocks: the 4 frames of a block of one pixel are 48 contiguous bytes, so a
+                    // lane's consecutive samples merge into the same L2 lines (12 B scattered per plane
+                    // became 32-B partial-line writes in HBM)
+                    const size_t at = (((size_t)(fp >> 2) * Q.lbuf_stride + local) * 4u + (fp & 3u)) * 3u;
+                    Q.lbuf[at] = L.x;
+                    Q.lbuf[at + 1] = L.y;
+                    Q.lbuf[at + 2] = L.z;
                 }
                 ++k;
-                if (k == lsu(LS_KEND)) {
+                if (k == min(Q.chunk_frames, Q.n_frames - kbase)) {
                     if (kbase == 0) {
-                        const float4 acc = make_float4(lsf(LS_ACC), lsf(LS_ACC + 1), lsf(LS_ACC + 2), lsf(LS_ACC + 3));
-                        P.accum[local] = acc;
-                        if (P.n_chunks == 1) {
-                            const float fr = (float)(P.first_frame + k - 1u);
+                        if (Q.n_chunks == 1) {
+                            const float fr = (float)(Q.first_frame + k - 1u);
                             const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
                             const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
-                            P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+                            Q.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
                         }
                     }
                     have_pixel = false;
@@ -424,36 +461,32 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
         const bool need = alive && !have_pixel;
         const uint64_t mask = __ballot(need);
         if (mask != 0) {
+            const KParams& Q = kargs();
             uint32_t base = 0;
             const int leader = __ffsll((unsigned long long)mask) - 1;
-            if ((int)lane == leader) base = atomicAdd(P.work_counter, (uint32_t)__popcll(mask));
+            if ((int)lane == leader) base = atomicAdd(Q.work_counter, (uint32_t)__popcll(mask));
             base = __shfl(base, leader);
             if (need) {
                 const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                if (w >= P.n_items) {
+                if (w >= Q.n_items) {
                     alive = false;
                 } else {
                     // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
-                    const uint32_t c = w / P.items_per_chunk, wp = w - c * P.items_per_chunk;
+                    const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
                     const uint32_t tile = wp >> 6, within = wp & 63u;
-                    const uint32_t trow = tile / P.tiles_x, tcol = tile - trow * P.tiles_x;
+                    const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
                     const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
-                    if (lr < P.n_local_rows && lx < P.W) {
+                    if (lr < Q.n_local_rows && lx < Q.W) {
                         // local row -> global row (row bands dealt round-robin over ranks)
-                        const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
-                        const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
-                        const uint32_t local = lr * P.W + lx;
-                        const uint32_t kbase = c * P.chunk_frames;
+                        const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+                        const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
+                        const uint32_t local = lr * Q.W + lx;
                         lsu(LS_LOCAL) = local;
                         lsu(LS_XY) = lx | (y << 16);
-                        lsu(LS_KBASE) = kbase;
-                        lsu(LS_KEND) = min(P.chunk_frames, P.n_frames - kbase);
+                        lsu(LS_C) = c;
                         have_pixel = true;
                         k = 0;
-                        if (!GB && c == 0) {
-                            const float4 a = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
-                            lsf(LS_ACC) = a.x; lsf(LS_ACC + 1) = a.y; lsf(LS_ACC + 2) = a.z; lsf(LS_ACC + 3) = a.w;
-                        }
+                        if (!GB && c == 0 && Q.first_frame == 1u) Q.accum[local] = make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                 }
             }
@@ -461,26 +494,27 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
 
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
+            const KParams& Q = kargs();
             const uint32_t xy = lsu(LS_XY), x = xy & 0xFFFFu, y = xy >> 16;
-            g.start(y * P.W + x, P.first_frame + lsu(LS_KBASE) + k);
+            g.start(y * Q.W + x, Q.first_frame + lsu(LS_C) * Q.chunk_frames + k);
             float cx, cy;
             if (GB) {   // centre of the pixel, DN/Camera.cpp:133
-                cx = ((float)x + 0.5f) / (float)P.W;
-                cy = ((float)y + 0.5f) / (float)P.H;
+                cx = ((float)x + 0.5f) / (float)Q.W;
+                cy = ((float)y + 0.5f) / (float)Q.H;
             } else {
                 const float ux = g.next();
                 const float uy = g.next();
-                cx = ((float)x + ux) / (float)P.W;
-                cy = ((float)y + uy) / (float)P.H;
+                cx = ((float)x + ux) / (float)Q.W;
+                cy = ((float)y + uy) / (float)Q.H;
             }
             cx = cx * 2.0f - 1.0f;
             cy = cy * 2.0f - 1.0f;
             float tg[4];
-            mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
+            mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
             const V3 dv = glm_normalize(divs(V3{tg[0], tg[1], tg[2]}, tg[3]));
             float wd[4];
-            mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
-            ray = make_ray(cam, w_normalize(V3{wd[0], wd[1], wd[2]}));
+            mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
+            ray = make_ray(V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]}, w_normalize(V3{wd[0], wd[1], wd[2]}));
             depth = 0;
             shadow = false;
             in_path = true;
@@ -507,26 +541,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             if (tracing) {
                 // box steps; up to two leaves are parked (in DFS order) before the lane stops
                 int parked0 = -1, parked1 = -1;
-                if (fin && P.variant == 1) {
-                    // predicated form: no per-lane branches inside the loop; a lane whose walk ended or
-                    // which holds two parked leaves keeps its state (selects), the wave leaves the loop
-                    // when no lane is active
-                    for (uint32_t s = 0; s < P.steps; ++s) {
-                        const bool act = ti < NN && parked1 < 0;
-                        if (!__any(act)) break;
-                        const uint32_t idx = act ? ti : 0u;
-                        const float4 q0 = S.nodes[2 * idx];
-                        const float4 q1 = S.nodes[2 * idx + 1];
-                        if (COUNT) { if (act) ++node_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_steps; }
-                        const bool hit = slab_hit_finite(ray, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
-                        const int tri = f2i(q1.w);
-                        const uint32_t nti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
-                        const bool leaf = act && hit && tri >= 0;
-                        ti = act ? nti : ti;
-                        parked1 = (leaf && parked0 >= 0) ? tri : parked1;
-                        parked0 = (leaf && parked0 < 0) ? tri : parked0;
-                    }
-                } else if (fin) {
+                if (fin) {
                     for (uint32_t s = 0; s < P.steps && ti < NN; ++s) {
                         const float4 q0 = S.nodes[2 * ti];
                         const float4 q1 = S.nodes[2 * ti + 1];
@@ -628,7 +643,7 @@ int occ_one(int block, size_t lds)
 
 size_t rt_stack_lds_bytes(uint32_t levels) { return (size_t)levels * 256 * (sizeof(float4) + 1); }
 
-size_t rt_lane_state_lds_bytes() { return (size_t)LS_WORDS * 256 * sizeof(float); }
+size_t rt_lane_state_lds_bytes(bool exact) { return (size_t)(exact ? LS_WORDS_EXACT : LS_WORDS_FAST) * 256 * sizeof(float); }
 
 size_t rt_scene_lds_bytes(const KParams& P)
 {
@@ -637,7 +652,7 @@ size_t rt_scene_lds_bytes(const KParams& P)
 
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream)
 {
-    const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes() + P.lds_pad;
+    const size_t sh = (lds ? rt_scene_lds_bytes(P) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes(exact || P.gb_color) + P.lds_pad;
     if (P.gb_color) {   // the Denoiser's G-buffer frame (EXACT, no counters)
         if (lds) hipLaunchKernelGGL((pt_megakernel<true, false, true, true>), dim3(grid), dim3(block), sh, stream, P);
         else hipLaunchKernelGGL((pt_megakernel<true, false, false, true>), dim3(grid), dim3(block), sh, stream, P);
@@ -673,19 +688,26 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
 
 // ---------------------------------------------------------------------------------------------
 // in-order completion of chunked pixels: accum (after chunk 0) += every later frame's sample in frame
-// order, then clamp + pack (MC/Renderer.cpp:128-133).  One thread per local pixel; the frame-major
-// buffer makes each frame's read coalesced across the pixels.
+// order, then clamp + pack (MC/Renderer.cpp:128-133).  One thread per local pixel; a 4-frame block is
+// three float4 loads, adjacent pixels' blocks adjacent (coalesced across the wave).
 __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_t n_px)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
     float4 acc = P.accum[i];
-    for (uint32_t f = P.chunk_frames; f < P.n_frames; ++f) {
-        const size_t at = (size_t)(f - P.chunk_frames) * P.lbuf_stride + i;
-        acc.x = acc.x + P.lbuf[at];
-        acc.y = acc.y + P.lbuf[at + P.lbuf_plane];
-        acc.z = acc.z + P.lbuf[at + 2 * P.lbuf_plane];
-        acc.w = acc.w + 1.0f;
+    const uint32_t nfp = P.n_frames - P.chunk_frames;
+    for (uint32_t b = 0; b * 4u < nfp; ++b) {
+        const float4* blk = reinterpret_cast<const float4*>(P.lbuf + ((size_t)b * P.lbuf_stride + i) * 12u);
+        const float4 q0 = blk[0], q1 = blk[1], q2 = blk[2];
+        const float v[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+        const uint32_t n = min(4u, nfp - b * 4u);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            if (j < n) {
+                acc.x = acc.x + v[3 * j]; acc.y = acc.y + v[3 * j + 1]; acc.z = acc.z + v[3 * j + 2];
+                acc.w = acc.w + 1.0f;
+            }
+        }
     }
     const float fr = (float)(P.first_frame + P.n_frames - 1u);
     const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);

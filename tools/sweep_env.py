@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of context-level knobs read from the environment at rt_create (RT_THRESH, RT_STEPS, RT_VARIANT,
+"""A/B of context-level knobs read from the environment at rt_create (RT_THRESH, RT_STEPS,
 RT_CHUNKS, RT_ITEMS_PER_LANE, RT_MIN_PX_PER_LANE) in ONE process, interleaved rounds, optionally on a
 row band of an N-rank frame (--rank/--nranks) to see multi-GPU per-rank behaviour on one GPU.
 
@@ -16,7 +16,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from _rt import rt  # noqa: E402
 
-KNOBS = ("RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_VARIANT", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE")
+KNOBS = ("RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES")
 
 
 def main():
@@ -59,7 +59,7 @@ def main():
                 res.append(c.stats().last_kernel_ms)
     for v, c, res in ctxs:
         ms = float(np.median(res))
-        print(json.dumps({"set": v, "rank": args.rank, "nranks": args.nranks, "kernel_ms": round(ms, 2), "n_chunks": c.stats().n_chunks, "grid": c.stats().grid,
+        print(json.dumps({"set": v, "rank": args.rank, "nranks": args.nranks, "kernel_ms": round(ms, 2), "all_ms": [round(x, 1) for x in res], "n_chunks": c.stats().n_chunks, "grid": c.stats().grid,
                           "msamples_per_s_rank": round(c.local_rows * W * spp / ms / 1e3, 1)}), flush=True)
         c.close()
 

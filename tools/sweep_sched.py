@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Sweep the megakernel's traversal scheduling knobs (RT_THRESH, RT_STEPS, RT_VARIANT; read at rt_create) in ONE
+"""Sweep the megakernel's traversal scheduling knobs (RT_THRESH, RT_STEPS; read at rt_create) in ONE
 process, interleaved rounds (cdna guide rule 24).  Prints one JSON line per setting.
 
     python tools/sweep_sched.py --thresh 8,16,24 --steps 8,12,16 --spp 64
@@ -24,7 +24,6 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--variant", default="0", help="RT_VARIANT values (comma list) to cross with the knobs")
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
     args = ap.parse_args()
@@ -35,14 +34,13 @@ def main():
         scene = rt.Scene.cornell()
     cam, _, _ = rt.camera_default(W, H)
     ctxs = {}
-    for va in args.variant.split(","):
-        for th in args.thresh.split(","):
-            for st in args.steps.split(","):
-                os.environ["RT_THRESH"], os.environ["RT_STEPS"], os.environ["RT_VARIANT"] = th, st, va
-                c = rt.Context(0)
-                c.upload(scene)
-                c.resize(W, H)
-                ctxs[(int(th), int(st), int(va))] = c
+    for th in args.thresh.split(","):
+        for st in args.steps.split(","):
+            os.environ["RT_THRESH"], os.environ["RT_STEPS"] = th, st
+            c = rt.Context(0)
+            c.upload(scene)
+            c.resize(W, H)
+            ctxs[(int(th), int(st))] = c
     res = {k: [] for k in ctxs}
     for r in range(args.rounds + 1):
         for k, c in ctxs.items():
@@ -51,7 +49,7 @@ def main():
             if r > 0:
                 res[k].append(W * H * spp / ms / 1e3)
     for k, v in res.items():
-        print(json.dumps({"thresh": k[0], "steps": k[1], "variant": k[2], "msamples_per_s": round(float(np.median(v)), 1),
+        print(json.dumps({"thresh": k[0], "steps": k[1], "msamples_per_s": round(float(np.median(v)), 1),
                           "fast": args.fast, "scene": args.scene}), flush=True)
     for c in ctxs.values():
         c.close()
