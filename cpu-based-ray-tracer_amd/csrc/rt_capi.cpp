@@ -26,7 +26,7 @@ struct rt_ctx {
     bool own_stream = false;
     std::string err;
     // scene
-    float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr;
+    float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr, *d_lboxes = nullptr;
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
@@ -65,6 +65,7 @@ struct rt_ctx {
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
+    bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
@@ -288,7 +289,9 @@ rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
     info->max_depth = h.max_depth;
     info->light_mesh = h.light_mesh;
     info->light_area = h.light_area;
-    info->device_bytes = (s->flat.nodes.size() + s->flat.tris.size() + s->flat.mats.size() + s->flat.lnodes.size() + s->flat.ltris.size()) * 4;
+    info->device_bytes = (s->flat.nodes.size() + s->flat.tris.size() + s->flat.mats.size() + s->flat.lnodes.size() + s->flat.ltris.size() +
+                          s->flat.lboxes.size()) * 4;
+    info->n_leaf_boxes = h.n_lboxes;
     return RT_OK;
 }
 
@@ -314,6 +317,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -364,7 +368,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_wmats); dfree(c->d_plights);
+    dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_lboxes); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
     dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf);
@@ -391,6 +395,7 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_mats, s->flat.mats)) != RT_OK) return r;
     if ((r = upload(c, c->d_lnodes, s->flat.lnodes)) != RT_OK) return r;
     if ((r = upload(c, c->d_ltris, s->flat.ltris)) != RT_OK) return r;
+    if ((r = upload(c, c->d_lboxes, s->flat.lboxes)) != RT_OK) return r;
     if ((r = upload(c, c->d_wmats, s->flat.wmats)) != RT_OK) return r;
     if ((r = upload(c, c->d_plights, s->flat.plights)) != RT_OK) return r;
     if ((r = upload(c, c->d_went, s->flat.went)) != RT_OK) return r;
@@ -444,6 +449,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.mats = c->d_mats; P.n_mats = c->hdr.n_mats;
     P.lnodes = c->d_lnodes; P.n_lnodes = c->hdr.n_lnodes;
     P.ltris = c->d_ltris; P.n_ltris = c->hdr.n_ltris;
+    P.lboxes = c->d_lboxes; P.n_lboxes = c->brute ? c->hdr.n_lboxes : 0;
     P.light_area = c->hdr.light_area;
     std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
     P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;

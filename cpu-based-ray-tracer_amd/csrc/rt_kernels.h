@@ -11,6 +11,7 @@ struct KParams {
     const float4* mats; uint32_t n_mats;
     const float4* lnodes; uint32_t n_lnodes;
     const float4* ltris; uint32_t n_ltris;
+    const float4* lboxes; uint32_t n_lboxes;   // small scenes: distinct leaf boxes + triangle masks (rt_layout.h)
     float light_area; float light_emission[3]; int has_light;
     // Whitted shading (rt_whitted.hip): per-material (diffuse color, phong_diffuse), point lights, sky
     const float4* wmats; const float4* plights; uint32_t n_plights; float sky[3];

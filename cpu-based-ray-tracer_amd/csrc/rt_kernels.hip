@@ -82,6 +82,7 @@ struct SceneView {
     const float4* lnodes;
     const float4* ltris;
     uint32_t n_nodes;
+    const float4* lboxes;   // small scenes: distinct leaf boxes (rt_layout.h), else unused
 };
 
 // One traversal: closest hit (shadow == false) or any blocking hit (shadow == true).
@@ -193,8 +194,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     SceneView S;
     S.n_nodes = P.n_nodes;
     if (LDS) {
-        // stage the whole scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris)
+        // stage the whole scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris | lboxes)
         const uint32_t nq = 2 * P.n_nodes, tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
+        const uint32_t bq = 2 * P.n_lboxes;
         float4* dn = lds_scene;
         float4* dt = dn + nq;
         float4* dm = dt + tq;
@@ -205,10 +207,12 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
         for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
         for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
         for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
+        float4* dbx = dlt + ltq;
+        for (uint32_t i = threadIdx.x; i < bq; i += blockDim.x) dbx[i] = P.lboxes[i];
         __syncthreads();
-        S.nodes = dn; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt;
+        S.nodes = dn; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt; S.lboxes = dbx;
     } else {
-        S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris;
+        S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = P.lboxes;
     }
 
     const uint32_t lane = __lane_id();
@@ -527,15 +531,54 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
         if (COUNT) { tc2 = clock64(); c_queue += tc2 - tc1; }
         if (!__any(have_pixel || alive)) break;
 
+        // ======================= small scenes: coherent trace =======================
+        // Every tracing lane tests every distinct leaf box -- the whole wave reads the same box, one
+        // uniform loop, no divergence -- then Moller-Trumbore on its candidate triangles in DFS order:
+        // exactly the triangles the reference's traversal tests (the leaf's slab test decides, see
+        // rt_scene.cpp), so the closest hit (ties: the later leaf) and the shadow verdict are the
+        // reference's.  A ray with a non-finite reciprocal direction (no monotone slab test) sends its
+        // wave through the BVH rounds below, run to completion.
+        bool coherent = false;
+        if (!COUNT && P.n_lboxes > 0) {
+            const bool tracing = in_path && !tdone;
+            coherent = __all(!tracing || rcp_finite(ray));
+            if (coherent && tracing) {
+                uint64_t cand = 0;
+                for (uint32_t b = 0; b < P.n_lboxes; ++b) {
+                    const float4 q0 = S.lboxes[2 * b], q1 = S.lboxes[2 * b + 1];
+                    if (slab_hit_finite(ray, q0.x, q0.y, q0.z, q1.x, q1.y, q1.z))
+                        cand |= (uint64_t)(uint32_t)f2i(q0.w) | ((uint64_t)(uint32_t)f2i(q1.w) << 32);
+                }
+                while (cand != 0) {
+                    const int tri = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
+                    double t;
+                    if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, ray, t)) {
+                        if (shadow) {
+                            if (!(slen < t + (double)0.01f)) { toccl = true; break; }   // MC/Renderer.cpp:184
+                        } else if (t <= tbest) {
+                            tbest = t; ttri = tri;   // the later leaf wins ties
+                        }
+                    }
+                }
+                ti = NN;
+                tdone = true;
+            }
+        }
+
         // ======================= traversal rounds =======================
         // Rounds continue while more than `thresh` lanes are still tracing, or while nobody waits for
         // service; then the finished lanes are served while the stragglers keep their traversal state.
+        // (Small scenes come here only for a non-finite ray: then every ray of the wave runs to the end.)
+        const uint32_t thresh = (!COUNT && P.n_lboxes > 0) ? 0u : P.thresh;
         for (;;) {
+            if (coherent) break;
             const bool tracing = in_path && !tdone;
             const uint64_t act = __ballot(tracing);
             if (act == 0) break;
             const uint64_t srv = __ballot((in_path && tdone) || (alive && !have_pixel));
-            if ((uint32_t)__popcll(act) <= P.thresh && srv != 0) break;
+            if ((uint32_t)__popcll(act) <= thresh && srv != 0) break;
             const bool fin = __all(!tracing || rcp_finite(ray));
             if (COUNT && lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_rounds;
             if (tracing) {
@@ -647,7 +690,7 @@ size_t rt_lane_state_lds_bytes(bool exact) { return (size_t)(exact ? LS_WORDS_EX
 
 size_t rt_scene_lds_bytes(const KParams& P)
 {
-    return (size_t)(2 * P.n_nodes + 4 * P.n_tris + 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris) * sizeof(float4);
+    return (size_t)(2 * P.n_nodes + 4 * P.n_tris + 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris + 2 * P.n_lboxes) * sizeof(float4);
 }
 
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream)
@@ -730,7 +773,7 @@ __global__ void __launch_bounds__(256) trace_kernel(KParams P, uint32_t n, const
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    SceneView S{P.nodes, P.tris, P.mats, P.lnodes, P.ltris, P.n_nodes};
+    SceneView S{P.nodes, P.tris, P.mats, P.lnodes, P.ltris, P.n_nodes, P.lboxes};
     const Ray r = make_ray(V3{org[3 * i], org[3 * i + 1], org[3 * i + 2]}, V3{dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]});
     uint32_t a = 0, b = 0;
     double best = 1.7976931348623157e308;

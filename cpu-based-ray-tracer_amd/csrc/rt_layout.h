@@ -54,7 +54,12 @@ typedef struct {
     uint32_t n_went, n_wtris;  // Whitted world (config C1): entities and mesh triangles
     int32_t max_bounce_depth;  // WH/World.h:55
     float intersection_correction;   // WH/World.h:56
+    uint32_t n_lboxes;         // distinct leaf boxes of a small scene (<= 64 triangles), 0 otherwise
 } rt_scene_header;
+
+// lboxes (small scenes, the megakernel's coherent trace): 2 float4 per distinct leaf box,
+// (lo.xyz, bits of the mask of its triangles 0-31)(hi.xyz, bits of the mask of triangles 32-63)
+#define RT_LBOX_QUADS 2
 
 #define RT_WENT_QUADS 4
 #define RT_WTRI_QUADS 4

@@ -402,6 +402,43 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         int32_t* e = &out.dbg_node_i[5 * (size_t)i];
         e[0] = n.left; e[1] = n.right; e[2] = n.tri; e[3] = n.mesh; e[4] = n.top;
     }
+    // ---- distinct leaf boxes of a small scene (the megakernel's coherent trace, rt_kernels.hip).
+    // The reference tests a triangle iff the slab test passes for its leaf box and every ancestor box
+    // (BVH::traverse_BVH_from_node, MC/BVH.h:82-101).  An ancestor box contains the leaf box exactly
+    // (checked here), and for a ray whose reciprocal direction is finite the slab test's correctly
+    // rounded subtractions and multiplications are monotone in the box planes, so an ancestor's entry
+    // distance is <= the leaf's and its exit distance >= the leaf's: the leaf's own test decides.
+    // Triangles with identical leaf boxes (the two halves of a quad) share one test.
+    out.lboxes.clear();
+    out.hdr.n_lboxes = 0;
+    if (NT > 0 && NT <= 64) {
+        bool contained = true;
+        std::vector<std::pair<Box, uint64_t>> uniq;
+        for (uint32_t i = 0; i < NN && contained; ++i) {
+            if (fn[i].tri < 0) continue;
+            const Box& lb = fn[i].box;
+            for (uint32_t j = 0; j < i; ++j) {
+                if (fn[j].tri >= 0 || fn[j].skip <= (int)i) continue;   // not an ancestor of leaf i
+                const Box& ab = fn[j].box;
+                if (!(ab.lo.x <= lb.lo.x && ab.lo.y <= lb.lo.y && ab.lo.z <= lb.lo.z && ab.hi.x >= lb.hi.x && ab.hi.y >= lb.hi.y &&
+                      ab.hi.z >= lb.hi.z)) { contained = false; break; }
+            }
+            size_t k = 0;
+            while (k < uniq.size() && std::memcmp(&uniq[k].first, &lb, sizeof(Box)) != 0) ++k;
+            if (k == uniq.size()) uniq.emplace_back(lb, 0ull);
+            uniq[k].second |= 1ull << fn[i].tri;
+        }
+        if (contained) {
+            out.hdr.n_lboxes = (uint32_t)uniq.size();
+            out.lboxes.resize(uniq.size() * 8);
+            for (size_t k = 0; k < uniq.size(); ++k) {
+                const Box& b = uniq[k].first;
+                float* q = &out.lboxes[8 * k];
+                q[0] = b.lo.x; q[1] = b.lo.y; q[2] = b.lo.z; q[3] = bits_as_float((int32_t)(uint32_t)uniq[k].second);
+                q[4] = b.hi.x; q[5] = b.hi.y; q[6] = b.hi.z; q[7] = bits_as_float((int32_t)(uint32_t)(uniq[k].second >> 32));
+            }
+        }
+    }
     out.tris.resize((size_t)NT * 16);
     out.dbg_tri_f.resize((size_t)NT * 13);
     out.dbg_tri_i.resize((size_t)NT * 2);

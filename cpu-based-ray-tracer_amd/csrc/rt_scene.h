@@ -47,6 +47,7 @@ struct FlatScene {
     rt_scene_header hdr{};
     std::vector<float> nodes, tris, mats, lnodes, ltris, wmats, plights;   // float4-granular
     std::vector<float> went, wtris;                                       // Whitted world (C1)
+    std::vector<float> lboxes;                                            // distinct leaf boxes (small scenes)
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag
     std::vector<float> dbg_node_f;    // 7 per node
     std::vector<int32_t> dbg_node_i;  // 5 per node

@@ -102,6 +102,7 @@ typedef struct {
     int32_t light_mesh;
     float light_area;
     uint64_t device_bytes; /* bytes the flattened scene occupies in HBM */
+    uint32_t n_leaf_boxes; /* distinct leaf boxes of a small scene's coherent trace (0: BVH traversal) */
 } rt_scene_info;
 rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 /* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node

@@ -135,3 +135,38 @@ def test_context_without_gpu_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(rt.RtError):
         rt.Context(0)
+
+
+def _leaf_boxes(nf, ni):
+    """Python restatement of the coherent trace's leaf boxes (rt_scene.cpp): distinct leaf boxes, and
+    whether every ancestor box contains its leaf's box (the condition for the leaf's slab test to decide)."""
+    n = nf.shape[0]
+    parent = np.full(n, -1)
+    for i in range(n):
+        if ni[i, 2] < 0:
+            parent[ni[i, 0]] = i
+            parent[ni[i, 1]] = i
+    uniq, contained = set(), True
+    for i in range(n):
+        if ni[i, 2] < 0:
+            continue
+        box = nf[i, :6]
+        uniq.add(box.tobytes())
+        j = parent[i]
+        while j >= 0:
+            a = nf[j, :6]
+            contained &= bool(np.all(a[:3] <= box[:3]) and np.all(a[3:] >= box[3:]))
+            j = parent[j]
+    return len(uniq), contained
+
+
+def test_small_scene_leaf_boxes():
+    """The Cornell box (32 triangles) traces through its distinct leaf boxes: every ancestor contains
+    its leaf's box, and the count matches the restatement; a scene over 64 triangles keeps the BVH."""
+    s = rt.Scene.cornell()
+    nf, ni, _, _ = s.export()
+    n, contained = _leaf_boxes(nf, ni)
+    assert contained and s.info().n_leaf_boxes == n and 0 < n <= 32
+    raw = np.load(os.path.join(G, "bvh_scene.npz"))["raw_bunny"]
+    big = rt.Scene.cornell_c5(raw)
+    assert big.info().n_tris > 64 and big.info().n_leaf_boxes == 0

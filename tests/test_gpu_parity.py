@@ -213,3 +213,27 @@ def test_full_size_matches_oracle(ctx, W, H, first, n):
     oacc, orgba, _ = O.Scene().render(W, H, n, seed=0, first_frame=first, threads=min(16, os.cpu_count() or 1))
     assert np.array_equal(bits(acc), bits(oacc))
     assert np.array_equal(rgba, orgba)
+
+
+def test_coherent_trace_equals_bvh_traversal(monkeypatch):
+    """Small scenes trace every ray through their distinct leaf boxes; RT_BRUTE=0 walks the BVH instead.
+    Same bits either way: a jittered frame, and a pixel-centre G-buffer frame whose centre ray is
+    exactly +z (a non-finite reciprocal direction, which sends its wave through the BVH rounds)."""
+    out = {}
+    for brute in ("1", "0"):
+        monkeypatch.setenv("RT_BRUTE", brute)
+        c = rt.Context(0)
+        try:
+            c.upload(rt.Scene.cornell())
+            c.resize(96, 64)
+            cam, _, _ = rt.camera_default(96, 64)
+            _, a = c.render(cam, 16, seed=9)
+            c.resize(65, 65)
+            cam, proj, view = rt.camera_look_ex(65, 65, (2.78, 2.73, -8.0), (0.0, 0.0, 1.0))
+            _, g = c.render_denoised(cam, proj, view, 1, rt.denoise_params(), seed=9)
+            gb = c.gbuffer()
+            out[brute] = (a, g, gb["color"], gb["position"], gb["normal"], gb["prim"])
+        finally:
+            c.close()
+    for x, y in zip(out["1"], out["0"]):
+        assert np.array_equal(bits(x), bits(y))
