@@ -147,7 +147,7 @@ def main():
         gat.gather()                                    # RCCL all-gather + reassembly on rank 0
         st = ctx.stats()
         kernel_ms.append(st.last_kernel_ms)
-        launch_info.update(passes=st.n_passes, chunks=st.n_chunks)
+        launch_info.update(passes=st.n_passes, chunks=st.n_chunks, kernel=rt.KERNEL_NAMES.get(st.kernel, str(st.kernel)))
 
     for _ in range(args.warmup):
         step()
@@ -182,7 +182,7 @@ def main():
     achieved = BYTES_PER_SAMPLE * per_launch / k_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "pt_megakernel", "kernel_ms": round(k_s * 1e3, 3),
+            "kernel": launch_info.get("kernel", "?"), "kernel_ms": round(k_s * 1e3, 3),
             "bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "samples_per_launch": int(per_launch),
             "launches_per_step": passes, "frame_chunks": int(launch_info.get("chunks", 1)),
             "gsamples_per_s_kernel": round(per_launch / k_s / 1e9, 4)}
@@ -190,7 +190,7 @@ def main():
     if os.path.exists(prof):
         try:
             pm = json.load(open(prof))
-            key = f"{W}x{H}x{spp}_{'fast' if args.fast else 'exact'}_n{world}_p{passes}"
+            key = f"{roof['kernel']}:{W}x{H}x{spp}_{'fast' if args.fast else 'exact'}_n{world}_p{passes}"
             if key in pm:
                 roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
         except Exception:

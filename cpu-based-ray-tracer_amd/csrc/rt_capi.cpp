@@ -66,6 +66,8 @@ struct rt_ctx {
     size_t lbuf_floats = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
+    bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
+    bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
 };
@@ -318,6 +320,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -354,6 +358,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
             c->occ_global[ex][cn] = b > 0 ? b : 2;
             if (ex) ex_max = std::max(ex_max, c->occ_global[ex][cn]);
         }
+    ex_max = std::max(ex_max, rt_coherent_occupancy(true, 256, 0));
     c->block = 256;
     // the EXACT fold stack is sized for the largest grid any mode launches (LDS staging never
     // raises occupancy above the register-limited value)
@@ -474,6 +479,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
     P.thresh = c->thresh; P.steps = c->steps;
+    P.force_walk = c->force_walk ? 1u : 0u;
     P.lds_pad = c->lds_pad;
     if (c->gb_next) {
         P.gb_color = c->d_gb_color; P.gb_pos = c->d_gb_pos; P.gb_nrm = c->d_gb_nrm; P.gb_prim = c->d_gb_prim; P.gb_clamp = c->gb_clamp;
@@ -482,18 +488,24 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const size_t lds_bytes = rt_scene_lds_bytes(P);
     const bool lds = (p->flags & RT_RENDER_GLOBAL_SCENE) == 0 && lds_bytes <= kMaxLdsScene;
     P.lds_scene_quads = lds ? (uint32_t)(lds_bytes / sizeof(float4)) : 0;
+    // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
+    const bool coh = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
+    auto occupancy = [&](size_t bytes) {
+        return coh ? rt_coherent_occupancy(exact, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
+    };
+    const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact) : rt_lane_state_lds_bytes(exact);
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
     if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
-        const size_t used = (lds ? lds_bytes : 0) + rt_lane_state_lds_bytes(exact) + c->lds_pad;
-        const int occ0 = rt_megakernel_occupancy(exact, count, lds, (int)c->block, used);
+        const size_t used = (lds ? lds_bytes : 0) + lane_bytes + c->lds_pad;
+        const int occ0 = occupancy(used);
         for (uint32_t lv = 8; lv > 0; --lv)
-            if (rt_megakernel_occupancy(exact, count, lds, (int)c->block, used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
+            if (occupancy(used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     if (exact && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
-    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + rt_lane_state_lds_bytes(exact) + c->lds_pad;
-    int bpc = rt_megakernel_occupancy(exact, count, lds, (int)c->block, shmem);
+    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
+    int bpc = occupancy(shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
@@ -553,7 +565,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local;
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
-                HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
+                if (coh) HIPC(c, rt_launch_coherent(Q, exact, grid, c->block, shmem, c->stream));
+                else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
                 HIPC(c, rt_launch_finalize_chunks(Q, (uint32_t)px_local, c->stream));
                 c->stats.n_chunks = n_chunks;
                 done += nf;
@@ -561,6 +574,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             c->stats.n_passes = passes;
         }
         c->stats.grid = grid;
+        c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);
         HIPC(c, hipEventRecord(c->ev1, c->stream));
         c->pending_stats = true;
     }

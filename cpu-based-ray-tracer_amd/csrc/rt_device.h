@@ -141,12 +141,12 @@ __device__ __forceinline__ bool rcp_finite(const Ray& r)
 // and barycentrics, strict inequalities).  A float sign pre-test rejects exactly the cases whose
 // double products cannot all be positive; a conservative |b2+b3| > |den| screen rejects cases the
 // double test would reject too; survivors run the reference's double arithmetic unchanged.
-__device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
+__device__ __forceinline__ bool moller_trumbore_od(const V3& a, const V3& e1, const V3& e2, const V3& o, const V3& d, double& t_out)
 {
-    const V3 S = sub(r.o, a);
-    const V3 S1 = cross(r.d, e2), S2 = cross(S, e1);
+    const V3 S = sub(o, a);
+    const V3 S1 = cross(d, e2), S2 = cross(S, e1);
     const float den = dot(S1, e1);
-    const float tn = dot(S2, e2), b2n = dot(S1, S), b3n = dot(S2, r.d);
+    const float tn = dot(S2, e2), b2n = dot(S1, S), b3n = dot(S2, d);
     const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
     const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
     if (!(pos || ngt)) return false;
@@ -157,6 +157,10 @@ __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const
     const double b3 = (double)b3n * inv;
     t_out = t;
     return (t > 0.0) && (b2 > 0.0) && (b3 > 0.0) && (((1.0 - b2) - b3) > 0.0);
+}
+__device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
+{
+    return moller_trumbore_od(a, e1, e2, r.o, r.d, t_out);
 }
 
 // cos/sin of the hemisphere angle phi = 2*PI*U in [0, 2*PI] (MC/WhittedMaterial.h:80-81 calls
@@ -247,7 +251,8 @@ __device__ __forceinline__ uint32_t to_u8(float v)
 }
 
 // glm mat4 * vec4, GLM/detail/type_mat4x4.inl:561-572: (m0*v0 + m1*v1) + (m2*v2 + m3*v3); m column-major
-__device__ __forceinline__ void mat4_mul(const float* m, float v0, float v1, float v2, float v3, float out[4])
+template <class PF>
+__device__ __forceinline__ void mat4_mul(PF m, float v0, float v1, float v2, float v3, float out[4])
 {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

@@ -42,6 +42,7 @@ struct KParams {
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
+    uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray
     unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
     // the Denoiser's G-buffer frame (set => pt_megakernel<..., GB = true>); one sample per pixel
     float4* gb_color; float4* gb_pos; float4* gb_nrm; int32_t* gb_prim; uint32_t gb_clamp;
@@ -54,6 +55,11 @@ size_t rt_stack_lds_bytes(uint32_t levels);
 size_t rt_lane_state_lds_bytes(bool exact);   // the megakernel's per-lane cold state (256 lanes)
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
+// small scenes (n_lboxes > 0, scene in LDS, no counters, no G-buffer): the vertex-synchronous kernel
+// (rt_coherent.hip); same KParams and LDS layout (scene | fold stack | lane state)
+hipError_t rt_launch_coherent(const KParams& P, bool exact, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
+int rt_coherent_occupancy(bool exact, int block, size_t lds_bytes);
+size_t rt_coherent_lane_state_lds_bytes(bool exact);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 // Whitted Style Ray Tracer world (spheres + textured meshes, reflection/refraction recursion), config C1

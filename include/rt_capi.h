@@ -185,7 +185,11 @@ typedef struct {
     uint32_t n_chunks;        /* frame chunks per pixel of the last rt_render's (last) launch: 1 unless the
                                  launch has few pixels per lane; last_kernel_ms covers the in-order finalize */
     uint32_t n_passes;        /* launches over consecutive frame ranges (bounded parked-sample memory) */
+    uint32_t kernel;          /* the path kernel of the last rt_render: RT_KERNEL_* */
 } rt_stats;
+#define RT_KERNEL_MEGA 0      /* pt_megakernel (rt_kernels.hip): any scene, counters, G-buffer frames */
+#define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */
+#define RT_KERNEL_WHITTED 2   /* whitted_kernel / whitted_world_kernel (rt_whitted.hip) */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 
 /* ------------------------------------------------------------------ the Denoiser (DN/ = Denoiser/8599RayTracerGUI/src/)

@@ -4,7 +4,7 @@ profiles/<round>/: per-launch PMC counters of the megakernel, HBM bytes per laun
 x 2, the gfx950 correction of MI355X_MICROARCH.md, + WRITE_SIZE x 1024), the kernel-trace statistics,
 and derived ratios.  Also updates profiles/pmc_traffic.json, which bench.py reads for `traffic`.
 
-    python profiles/summarize_pmc.py gpurun_out/prof_r01 profiles/r01 --key 1920x1080x1024_exact_n1_p1 --samples 2123366400
+    python profiles/summarize_pmc.py gpurun_out/prof_r01 profiles/r01 --key 1920x1080x1024_exact_n1_p1 --samples 2123366400 --kernel pt_coherent_kernel
 """
 import argparse
 import collections
@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("dst")
-    ap.add_argument("--key", required=True, help="bench.py traffic key (WxHxSPP_mode_nN_pP)")
+    ap.add_argument("--key", required=True, help="bench.py traffic key (WxHxSPP_mode_nN_pP; stored as KERNEL:key)")
     ap.add_argument("--samples", type=float, required=True, help="samples per megakernel launch")
     ap.add_argument("--kernel", default="pt_megakernel")
     args = ap.parse_args()
@@ -43,7 +43,7 @@ def main():
         out["hbm_bytes_per_sample"] = hbm / args.samples
         tj = os.path.join(os.path.dirname(os.path.abspath(__file__)), "pmc_traffic.json")
         traffic = json.load(open(tj)) if os.path.exists(tj) else {}
-        traffic[args.key] = {"hbm_bytes_per_launch": hbm, "source": os.path.join(args.dst, "pmc_summary.json")}
+        traffic[args.kernel + ":" + args.key] = {"hbm_bytes_per_launch": hbm, "source": os.path.join(args.dst, "pmc_summary.json")}
         json.dump(traffic, open(tj, "w"), indent=1)
     for name in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
         if name in counters:

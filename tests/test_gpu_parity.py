@@ -237,3 +237,31 @@ def test_coherent_trace_equals_bvh_traversal(monkeypatch):
             c.close()
     for x, y in zip(out["1"], out["0"]):
         assert np.array_equal(bits(x), bits(y))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exact", [True, False])
+def test_vertex_kernel_equals_megakernel(monkeypatch, exact):
+    """Small scenes render with the vertex-synchronous kernel (rt_coherent.hip); RT_VERTEX=0 runs the
+    general megakernel, RT_FORCE_WALK=1 sends every ray of the vertex kernel through its per-lane BVH
+    walk (the path of rays with a non-finite reciprocal direction).  Same bits in EXACT and FAST mode,
+    with and without frame chunks."""
+    out = {}
+    for name, env in (("vertex", {}), ("mega", {"RT_VERTEX": "0"}), ("walk", {"RT_FORCE_WALK": "1"}),
+                      ("vertex_chunks", {"RT_CHUNKS": "3"})):
+        for k in ("RT_VERTEX", "RT_FORCE_WALK", "RT_CHUNKS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = rt.Context(0)
+        try:
+            c.upload(rt.Scene.cornell())
+            c.resize(80, 56)
+            cam, _, _ = rt.camera_default(80, 56)
+            rgba, a = c.render(cam, 24, seed=5, exact=exact)
+            out[name] = (rgba, a)
+        finally:
+            c.close()
+    for name in ("mega", "walk", "vertex_chunks"):
+        assert np.array_equal(out[name][0], out["vertex"][0]), name
+        assert np.array_equal(bits(out[name][1]), bits(out["vertex"][1])), name
