@@ -51,6 +51,8 @@ class Stats(C.Structure):
                 ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
                 ("n_passes", C.c_uint32), ("kernel", C.c_uint32)]
 
+_DIAGNOSTIC = {"rt_debug_counters"}
+
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel"}
 
 
@@ -118,6 +120,7 @@ def lib():
         "rt_reset_accumulation": (i32, [vp]),
         "rt_synchronize": (i32, [vp]),
         "rt_get_stats": (i32, [vp, C.POINTER(Stats)]),
+        "rt_debug_counters": (i32, [vp, C.POINTER(C.c_uint64), u32]),
         "rt_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(C.c_double)]),
         "rt_math_selftest": (i32, [vp, u64, fp, fp]),
         "rt_world_material_default": (None, [C.POINTER(WorldMaterial)]),
@@ -132,6 +135,8 @@ def lib():
         "rt_get_gbuffer": (i32, [vp, fp, fp, fp, C.POINTER(i32), fp]),
     }
     for name, (res, args) in sig.items():
+        if name in _DIAGNOSTIC and not hasattr(L, name):
+            continue   # diagnostics only (A/B against older builds)
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -412,6 +417,12 @@ class Context:
         s = Stats()
         self._check(lib().rt_get_stats(self.h, C.byref(s)), "rt_get_stats")
         return s
+
+    def debug_counters(self, n=32):
+        """Raw device counters of the last render (diagnostics; rt_debug_counters)."""
+        out = (C.c_uint64 * n)()
+        self._check(lib().rt_debug_counters(self.h, out, n), "rt_debug_counters")
+        return list(out)
 
     def sync(self):
         self._check(lib().rt_synchronize(self.h), "rt_synchronize")

@@ -493,17 +493,17 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };
-    const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact) : rt_lane_state_lds_bytes(exact);
+    const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0) : rt_lane_state_lds_bytes(exact);
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
-    if (exact && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {
+    if (exact && !coh && (p->flags & RT_RENDER_GLOBAL_STACK) == 0) {   // the vertex kernel's fold ring is in HBM
         const size_t used = (lds ? lds_bytes : 0) + lane_bytes + c->lds_pad;
         const int occ0 = occupancy(used);
         for (uint32_t lv = 8; lv > 0; --lv)
             if (occupancy(used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
-    if (exact && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
+    if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
     const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
@@ -535,8 +535,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     want = (uint32_t)std::min<uint64_t>({(uint64_t)p->n_frames, std::max<uint64_t>(1, p->n_frames / c->min_chunk_frames),
                                                          ((uint64_t)c->items_per_lane * lanes + px_local - 1) / px_local});
             }
+            // the vertex kernel parks every frame (finalize accumulates them); the megakernel parks the
+            // frames of chunks >= 1
+            const bool park_all = coh;
             uint32_t passes = 1;
-            if (want > 1) {
+            if (want > 1 || park_all) {
                 const uint64_t bytes = px_local * (uint64_t)p->n_frames * 12ull;
                 passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
             }
@@ -550,11 +553,12 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 const uint32_t F = (nf + n_chunks - 1) / n_chunks;
                 n_chunks = (nf + F - 1) / F;
                 Q.n_chunks = n_chunks; Q.chunk_frames = F; Q.items_per_chunk = (uint32_t)items_px;
+                Q.park_all = park_all ? 1u : 0u;
                 if (items_px * n_chunks >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
                 Q.n_items = (uint32_t)(items_px * n_chunks);
-                if (n_chunks > 1) {
+                if (n_chunks > 1 || park_all) {
                     // 4-frame blocks of 12 floats per pixel (rt_kernels.hip)
-                    const size_t plane = (size_t)px_local * (((nf - F) + 3u) & ~3u);
+                    const size_t plane = (size_t)px_local * (((park_all ? nf : nf - F) + 3u) & ~3u);
                     if (3 * plane > c->lbuf_floats) {
                         HIPC(c, hipStreamSynchronize(c->stream));
                         dfree(c->d_lbuf);
@@ -710,6 +714,14 @@ rt_status rt_synchronize(rt_ctx* c)
 {
     if (!c) return RT_ERR_INVALID;
     HIPC(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+rt_status rt_debug_counters(rt_ctx* c, uint64_t* out, uint32_t n)
+{
+    if (!c || !out || n > 32) return RT_ERR_INVALID;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    HIPC(c, hipMemcpy(out, c->d_counters, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -36,12 +36,25 @@ namespace {
 // per-lane cold state in LDS, [field][lane] words
 enum : uint32_t {
     VS_LOCAL = 0, VS_XY = 1, VS_C = 2,   // the work item: local pixel, (x, y) global, frame chunk
-    VS_RNG = 3,                          // the Philox block of the current 4 draws (4 words)
-    VS_LD = 7,                           // the pending vertex's unoccluded direct term (3 words)
-    VS_PCOS = 10, VS_MAT = 11,           // the pending vertex's indirect cosine and material
-    VS_PIX = 12, VS_FRAME = 13,          // the sample's stream counter (pixel, frame)
-    VS_THR = 14, VS_LSUM = 17,           // FAST: throughput, radiance
-    VS_WORDS_EXACT = 14, VS_WORDS_FAST = 20
+    VS_PIX = 3, VS_FRAME = 4,            // the sample's stream counter (pixel, frame)
+    VS_LD = 5,                           // the pending vertex's unoccluded direct term (3 words)
+    VS_PCOS = 8, VS_MAT = 9,             // the pending vertex's indirect cosine and material
+    VS_BASE = 10,                        // EXACT: ring position of the current path's level 0
+    VS_DL = 11,                          // EXACT drain: the partial fold (3 words)
+    VS_DPOS = 14,                        // EXACT drain: ring position of the next level to fold
+    VS_DT0 = 15, VS_DT1 = 16,            // EXACT drain: the sample's local pixel and frame index
+    VS_THR = 10, VS_LSUM = 13,           // FAST: throughput, radiance
+    VS_WORDS_EXACT = 17, VS_WORDS_FAST = 16,
+    VS_RNG = 17,                         // unlit scenes only: the Philox block of the current 4 draws
+    VS_WORDS_UNLIT = 21
+};
+
+// The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
+// sample_hemisphere (straight-line code: the index folds to constants)
+struct FixedDraws {
+    float u[6];
+    int i;
+    __device__ __forceinline__ float next() { return u[i++]; }
 };
 
 // The lane's uniform draws (rt_path.h LaneRng) with only the draw index in a register: the counter
@@ -51,7 +64,6 @@ struct VertexRng {
     uint32_t* w;        // the lane's word 0 of the cold state (stride 256)
     uint32_t k0, k1;    // key (uniform)
     uint32_t dim;
-    __device__ __forceinline__ void start(uint32_t px, uint32_t fr) { w[VS_PIX * 256u] = px; w[VS_FRAME * 256u] = fr; dim = 0; }
     __device__ __forceinline__ float next()
     {
         if ((dim & 3u) == 0u) {
@@ -62,6 +74,37 @@ struct VertexRng {
         const uint32_t u = w[(VS_RNG + (dim & 3u)) * 256u];
         ++dim;
         return (float)u / 4294967296.0f;   // Walnut::Random::Float, (float)UINT32_MAX == 2^32 exactly
+    }
+    // A vertex of a lit scene draws dims d .. d+5 with d = 2 + 6 * vertex (2 camera draws, then 3 light
+    // + roulette + 2 hemisphere per vertex), so d % 4 is 0 or 2 and the six draws lie in the two
+    // Philox blocks d/4 and d/4 + 1: every vertex lane evaluates exactly those two blocks, in lockstep,
+    // instead of one block wherever its own draw index crosses a multiple of 4 (which, with lanes at
+    // different vertices, made every draw site run Philox for some lane).
+    __device__ __forceinline__ void vertex_draws(FixedDraws& fd)
+    {
+        const uint32_t b = dim >> 2;
+        uint32_t o[8];
+        philox4x32_10(w[VS_PIX * 256u], w[VS_FRAME * 256u], b, 0u, k0, k1, o);
+        philox4x32_10(w[VS_PIX * 256u], w[VS_FRAME * 256u], b + 1u, 0u, k0, k1, o + 4);
+        // words (o[0..5] or o[2..7]) picked by a mask, not by an index: a select the compiler turns
+        // into a dynamic array offset puts o[] in scratch memory
+        const uint32_t msk = (dim & 2u) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) fd.u[i] = (float)(o[i] ^ ((o[i] ^ o[i + 2]) & msk)) / 4294967296.0f;
+        fd.i = 0;
+        dim += 6u;
+    }
+    // the camera draws: dims 0 and 1 of block 0 (the block is kept in LDS only for unlit scenes,
+    // whose vertices draw through next())
+    __device__ __forceinline__ void camera_draws(uint32_t px, uint32_t fr, bool keep, float& ux, float& uy)
+    {
+        w[VS_PIX * 256u] = px; w[VS_FRAME * 256u] = fr;
+        uint32_t o[4];
+        philox4x32_10(px, fr, 0u, 0u, k0, k1, o);
+        if (keep) { w[VS_RNG * 256u] = o[0]; w[(VS_RNG + 1) * 256u] = o[1]; w[(VS_RNG + 2) * 256u] = o[2]; w[(VS_RNG + 3) * 256u] = o[3]; }
+        ux = (float)o[0] / 4294967296.0f;
+        uy = (float)o[1] / 4294967296.0f;
+        dim = 2;
     }
 };
 
@@ -83,17 +126,34 @@ __device__ __forceinline__ bool box_hit(const V3& s0, const V3& s1, const V3& rc
     return (tout >= 0.0f) && (tin <= tout);
 }
 
-__device__ __forceinline__ V3 rcp3(V3 d) { return V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z}; }
+__device__ __forceinline__ V3 rcp3(V3 d) { return V3{rcp_f32(d.x), rcp_f32(d.y), rcp_f32(d.z)}; }
 __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
 }  // namespace
 
-#ifndef RT_MIN_WAVES
-#define RT_MIN_WAVES 1
+// minimum waves per SIMD the register allocation must admit: 7 (72 VGPRs) fits without spilling VGPRs
+#ifndef RT_COH_MIN_WAVES
+#define RT_COH_MIN_WAVES 7
+#endif
+// cost attribution (A/B builds, tools/ab_libs.py): run the leaf-box loop / the Moller-Trumbore loop
+// this many times per trace step (extra runs' results are discarded; the image is unchanged)
+#ifndef RT_REP_BOX
+#define RT_REP_BOX 1
+#endif
+#ifndef RT_REP_MT
+#define RT_REP_MT 1
+#endif
+// section timing (diagnostic builds): wave cycles spent in service-head / vertex / finish / queue /
+// camera / box loop / Moller-Trumbore, summed into counters[16..23]
+#ifndef RT_SECTIONS
+#define RT_SECTIONS 0
+#endif
+#ifndef RT_PAD_VALU
+#define RT_PAD_VALU 0
 #endif
 
 template <bool EXACT>
-__global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams P)
+__global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
     SceneView S;
@@ -118,15 +178,44 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
     const uint32_t lane = __lane_id();
     const uint32_t gtid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t tib = threadIdx.x;
-    // EXACT fold stack: levels [0, lds_levels) in LDS ([level][lane] float4 + u8 material), deeper in HBM
-    float4* lstack = lds_scene + P.lds_scene_quads;
-    uint8_t* lmat = reinterpret_cast<uint8_t*>(lstack + (size_t)P.lds_levels * 256);
-    float* lstate = reinterpret_cast<float*>(lmat + (size_t)P.lds_levels * 256u);
+    // the lane's cold state after the scene (the host gives this kernel no LDS fold levels)
+    float* lstate = reinterpret_cast<float*>(lds_scene + P.lds_scene_quads);
     auto lsf = [&](uint32_t f) -> float& { return lstate[f * 256u + tib]; };
     auto lsu = [&](uint32_t f) -> uint32_t& { return reinterpret_cast<uint32_t*>(lstate)[f * 256u + tib]; };
     auto ls3 = [&](uint32_t f) { return V3{lsf(f), lsf(f + 1), lsf(f + 2)}; };
     auto st3 = [&](uint32_t f, V3 v) { lsf(f) = v.x; lsf(f + 1) = v.y; lsf(f + 2) = v.z; };
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
+    // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
+    // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
+    // pixel's samples in frame order (MC/Renderer.cpp:128-133).  The kernel issues no global load
+    // after a store of the same iteration: on gfx950 a load waits for every older store of its wave
+    // (vmcnt counts both), and a path-tracing iteration that read the accumulator after its parked
+    // samples and fold-level stores waited for their write-back.
+    auto complete = [&](V3 L, uint32_t local, uint32_t fidx) {
+        CKParams& Q = kargs4();
+        const size_t at = (((size_t)(fidx >> 2) * Q.lbuf_stride + local) * 4u + (fidx & 3u)) * 3u;
+        Q.lbuf[at] = L.x;
+        Q.lbuf[at + 1] = L.y;
+        Q.lbuf[at + 2] = L.z;
+    };
+    // one fold step of the draining path: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
+    // (MC/Renderer.cpp:208,213), inner level first
+    auto drain_step = [&](uint32_t& dleft) {
+        CKParams& Q = kargs4();
+        const uint32_t pos = lsu(VS_DPOS);
+        const float4 e = Q.stack_ld[(size_t)pos * Q.total_threads + gtid];
+        const int m = Q.stack_mat[(size_t)pos * Q.total_threads + gtid];
+        const float4 mb2 = S.mats[2 * m];
+        const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
+        const V3 L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(ls3(VS_DL), f), e.w), PDF), Q.rr));
+        dleft = dleft - 1u;
+        if (dleft == 0u) {
+            complete(L, lsu(VS_DT0), lsu(VS_DT1));
+        } else {
+            st3(VS_DL, L);
+            lsu(VS_DPOS) = (pos == 0u ? Q.stack_depth : pos) - 1u;
+        }
+    };
 
     bool alive = true, have_pixel = false, in_path = false;
     uint32_t k = 0;       // frame of the current item (item of chunk c: frames c * chunk_frames + [0, kend))
@@ -143,8 +232,81 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
     int triA = -1;                            // closest triangle
     bool occB = false;                        // shadow ray blocked
+    // EXACT: a finished path's levels are folded one per iteration ("drain"), not in a loop at the end of
+    // the path: lanes end paths of different depths, and a fold loop runs as long as the deepest one.
+    // Levels live in a per-lane ring of stack_depth positions in HBM ([position][thread]); the next path
+    // pushes above the draining segment.  A sample is accumulated when its fold completes; a path that
+    // ends while the previous fold still drains first completes that fold, so the per-pixel order of the
+    // accumulation is the frame order.
+    uint32_t dleft = 0;                       // levels of the draining fold still to apply
+    if (EXACT) lsu(VS_BASE) = 0u;
 
+#if RT_SECTIONS
+    uint64_t sec_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t sec_t = clock64();
+    int sec_cur = 7;
+#define SEC_MARK(k) do { const uint64_t t_ = clock64(); sec_cyc[sec_cur] += t_ - sec_t; sec_t = t_; sec_cur = (k); } while (0)
+    // lane activity: [0] wave iterations, [1] lanes on a path, [2] vertex lanes, [3] finishing lanes,
+    // [4] camera lanes, [5] MT loop wave iterations, [6] MT tests (lanes), [7] fold wave iterations
+    uint64_t sec_n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool dbg_vertex = false, dbg_fin = false, dbg_cam = false;
+#define SEC_COUNT(i, v) do { sec_n[i] += (v); } while (0)
+#else
+#define SEC_COUNT(i, v) do { } while (0)
+#define SEC_MARK(k) do { } while (0)
+#endif
     for (;;) {
+        SEC_MARK(0);
+#if RT_PAD_VALU
+        {   // diagnostic: RT_PAD_VALU independent VALU ops per iteration (VALU-throughput sensitivity)
+            float a0 = (float)lane, a1 = a0 + 1.0f, a2 = a0 + 2.0f, a3 = a0 + 3.0f;
+#pragma unroll
+            for (int i = 0; i < RT_PAD_VALU / 4; ++i) {
+                asm volatile("v_add_f32 %0, 1.0, %0\n v_add_f32 %1, 1.0, %1\n v_add_f32 %2, 1.0, %2\n v_add_f32 %3, 1.0, %3"
+                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
+            }
+            asm volatile("" : : "v"(a0), "v"(a1), "v"(a2), "v"(a3));
+        }
+#endif
+        if (EXACT && __any(dleft != 0u)) {
+            if (dleft != 0u) drain_step(dleft);
+        }
+        // ======================= lane-level work queue (wave-collective) =======================
+        // at the top of the iteration, before any store: a lane that finished its item in the previous
+        // iteration takes the next one (the returning atomic waits for no store of this iteration)
+        const bool need = alive && !have_pixel;
+        const uint64_t mask = __ballot(need);
+        if (mask != 0) {
+            CKParams& Q = kargs4();
+            uint32_t base = 0;
+            const int leader = __ffsll((unsigned long long)mask) - 1;
+            if ((int)lane == leader) base = atomicAdd(Q.work_counter, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                if (w >= Q.n_items) {
+                    alive = false;
+                } else {
+                    // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
+                    const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
+                    const uint32_t tile = wp >> 6, within = wp & 63u;
+                    const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
+                    const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
+                    if (lr < Q.n_local_rows && lx < Q.W) {
+                        // local row -> global row (row bands dealt round-robin over ranks)
+                        const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+                        const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
+                        const uint32_t local = lr * Q.W + lx;
+                        lsu(VS_LOCAL) = local;
+                        lsu(VS_XY) = lx | (y << 16);
+                        lsu(VS_C) = c;
+                        have_pixel = true;
+                        k = 0;
+                    }
+                }
+            }
+        }
+
         // ======================= service: every lane on a path has its rays back =======================
         if (in_path) {
             CKParams& Q = kargs4();
@@ -188,12 +350,19 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                     const uint32_t lvl = depth - 1;
                     const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
                     const uint32_t pm = lsu(VS_MAT);
-                    if (lvl < Q.lds_levels) {
-                        lstack[lvl * 256u + tib] = e;
-                        lmat[lvl * 256u + tib] = (uint8_t)pm;
-                    } else if (lvl < Q.stack_depth) {
-                        Q.stack_ld[(size_t)lvl * Q.total_threads + gtid] = e;
-                        Q.stack_mat[(size_t)lvl * Q.total_threads + gtid] = pm;
+                    const uint32_t R = Q.stack_depth;
+                    uint32_t pos = lsu(VS_BASE) + lvl;
+                    if (pos >= R) pos -= R;
+                    // the ring holds this path's levels above the draining ones, which occupy the R positions
+                    // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
+                    bool fits = lvl < R;
+                    if (fits && dleft != 0u) {
+                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
+                        fits = (pos + R - lo) % R >= dleft;
+                    }
+                    if (fits) {
+                        Q.stack_ld[(size_t)pos * Q.total_threads + gtid] = e;
+                        Q.stack_mat[(size_t)pos * Q.total_threads + gtid] = pm;
                     } else {
                         atomicAdd((unsigned long long*)&Q.counters[3], 1ull);   // reported as stack overflow
                     }
@@ -210,6 +379,10 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                 vertex = true;
             }
 
+            SEC_MARK(1);
+#if RT_SECTIONS
+            dbg_vertex = vertex; dbg_fin = finished;
+#endif
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
                 const float4 tq3 = S.tris[4 * triA + 3];
@@ -218,30 +391,39 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                 const V3 N{tq3.x, tq3.y, tq3.z};
                 const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
                 const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
-                hasB = false;
+                auto shade = [&](auto& G) {
+                    hasB = false;
+                    if (Q.has_light) {
+                        V3 q, nl0;
+                        sample_light(S, Q.light_area, G, q, nl0);
+                        const V3 p2q = sub(q, p);
+                        const V3 wl = glm_normalize(p2q);
+                        const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
+                        const float sc1 = dot(wl, n), sc2 = dot(neg(wl), nl), sd2 = dot(p2q, p2q);
+                        slen = glm_length(p2q);
+                        // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
+                        const float4 mb = S.mats[2 * mat];
+                        const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
+                        st3(VS_LD, divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2),
+                                        (1.0f / Q.light_area)));
+                        dB = wl; rB = rcp3(wl);
+                        hasB = true;
+                    }
+                    // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
+                    cont = G.next() < Q.rr && depth < 4096u;
+                    if (cont) {
+                        const V3 wi = glm_normalize(sample_hemisphere(n, G));
+                        lsf(VS_PCOS) = dot(wi, n);
+                        lsu(VS_MAT) = (uint32_t)mat;
+                        dA = wi; rA = rcp3(wi);
+                    }
+                };
                 if (Q.has_light) {
-                    V3 q, nl0;
-                    sample_light(S, Q.light_area, g, q, nl0);
-                    const V3 p2q = sub(q, p);
-                    const V3 wl = glm_normalize(p2q);
-                    const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
-                    const float sc1 = dot(wl, n), sc2 = dot(neg(wl), nl), sd2 = dot(p2q, p2q);
-                    slen = glm_length(p2q);
-                    // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
-                    const float4 mb = S.mats[2 * mat];
-                    const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                    st3(VS_LD, divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2),
-                                    (1.0f / Q.light_area)));
-                    dB = wl; rB = rcp3(wl);
-                    hasB = true;
-                }
-                // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
-                cont = g.next() < Q.rr && depth < 4096u;
-                if (cont) {
-                    const V3 wi = glm_normalize(sample_hemisphere(n, g));
-                    lsf(VS_PCOS) = dot(wi, n);
-                    lsu(VS_MAT) = (uint32_t)mat;
-                    dA = wi; rA = rcp3(wi);
+                    FixedDraws fd;
+                    g.vertex_draws(fd);
+                    shade(fd);
+                } else {
+                    shade(g);
                 }
                 hasA = cont;
                 o = p;
@@ -249,96 +431,54 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                 depth = depth + 1;
             }
 
+            SEC_MARK(2);
             if (finished) {
-                if (EXACT) {
-                    // fold inner-first: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)   (MC/Renderer.cpp:208,213)
-                    for (int lvl = fold_top; lvl >= 0; --lvl) {
-                        float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-                        int m = 0;
-                        if ((uint32_t)lvl < Q.lds_levels) {
-                            e = lstack[(uint32_t)lvl * 256u + tib];
-                            m = lmat[(uint32_t)lvl * 256u + tib];
-                        } else if ((uint32_t)lvl < Q.stack_depth) {
-                            e = Q.stack_ld[(size_t)lvl * Q.total_threads + gtid];
-                            m = Q.stack_mat[(size_t)lvl * Q.total_threads + gtid];
-                        }
-                        const float4 mb2 = S.mats[2 * m];
-                        const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                        L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(L, f), e.w), PDF), Q.rr));
-                    }
-                }
                 in_path = false;
                 hasA = hasB = false;
                 const uint32_t local = lsu(VS_LOCAL), kbase = lsu(VS_C) * Q.chunk_frames;
-                float4 acc;
-                if (kbase == 0) {
-                    // chunk 0: temporal accumulation + clamp + pack (MC/Renderer.cpp:128-133), in place
-                    acc = Q.accum[local];
-                    acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z; acc.w = acc.w + 1.0f;
-                    Q.accum[local] = acc;
-                } else {
-                    // a later chunk: the sample waits in 4-frame blocks for finalize_chunks_kernel
-                    const uint32_t fp = kbase + k - Q.chunk_frames;
-                    const size_t at = (((size_t)(fp >> 2) * Q.lbuf_stride + local) * 4u + (fp & 3u)) * 3u;
-                    Q.lbuf[at] = L.x;
-                    Q.lbuf[at + 1] = L.y;
-                    Q.lbuf[at + 2] = L.z;
-                }
+                const uint32_t fidx = kbase + k;   // the sample's frame index in this launch
                 ++k;
-                if (k == min(Q.chunk_frames, Q.n_frames - kbase)) {
-                    if (kbase == 0 && Q.n_chunks == 1) {
-                        const float fr = (float)(Q.first_frame + k - 1u);
-                        const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
-                        const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
-                        Q.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+                const bool last = k == min(Q.chunk_frames, Q.n_frames - kbase);
+                if (last) have_pixel = false;
+                if (EXACT) {
+#if RT_SECTIONS
+                    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(7, 1);
+#endif
+                    while (dleft != 0u) drain_step(dleft);   // the previous sample's fold completes first
+                    const uint32_t m = (uint32_t)(fold_top + 1);
+                    const uint32_t base = lsu(VS_BASE);
+                    if (m == 0u) {
+                        complete(L, local, fidx);
+                    } else {
+                        // the fold drains from the innermost level, ring position base + m - 1
+                        st3(VS_DL, L);
+                        uint32_t top = base + m - 1u;
+                        if (top >= Q.stack_depth) top -= Q.stack_depth;
+                        lsu(VS_DPOS) = top;
+                        lsu(VS_DT0) = local;
+                        lsu(VS_DT1) = fidx;
+                        dleft = m;
+                        uint32_t nb = top + 1u;
+                        if (nb >= Q.stack_depth) nb -= Q.stack_depth;
+                        lsu(VS_BASE) = nb;   // the next path pushes above the draining levels
                     }
-                    have_pixel = false;
-                }
-            }
-        }
-
-        // ======================= lane-level work queue (wave-collective) =======================
-        const bool need = alive && !have_pixel;
-        const uint64_t mask = __ballot(need);
-        if (mask != 0) {
-            CKParams& Q = kargs4();
-            uint32_t base = 0;
-            const int leader = __ffsll((unsigned long long)mask) - 1;
-            if ((int)lane == leader) base = atomicAdd(Q.work_counter, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                if (w >= Q.n_items) {
-                    alive = false;
                 } else {
-                    // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
-                    const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
-                    const uint32_t tile = wp >> 6, within = wp & 63u;
-                    const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
-                    const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
-                    if (lr < Q.n_local_rows && lx < Q.W) {
-                        // local row -> global row (row bands dealt round-robin over ranks)
-                        const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
-                        const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
-                        const uint32_t local = lr * Q.W + lx;
-                        lsu(VS_LOCAL) = local;
-                        lsu(VS_XY) = lx | (y << 16);
-                        lsu(VS_C) = c;
-                        have_pixel = true;
-                        k = 0;
-                        if (c == 0 && Q.first_frame == 1u) Q.accum[local] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    }
+                    complete(L, local, fidx);
                 }
             }
         }
 
+        SEC_MARK(3);
+        SEC_MARK(4);
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
             CKParams& Q = kargs4();
             const uint32_t xy = lsu(VS_XY), x = xy & 0xFFFFu, y = xy >> 16;
-            g.start(y * Q.W + x, Q.first_frame + lsu(VS_C) * Q.chunk_frames + k);
-            const float ux = g.next();
-            const float uy = g.next();
+            float ux, uy;
+            g.camera_draws(y * Q.W + x, Q.first_frame + lsu(VS_C) * Q.chunk_frames + k, !Q.has_light, ux, uy);
+#if RT_SECTIONS
+            dbg_cam = true;
+#endif
             float cx = ((float)x + ux) / (float)Q.W;
             float cy = ((float)y + uy) / (float)Q.H;
             cx = cx * 2.0f - 1.0f;
@@ -358,14 +498,27 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
             if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
         }
 
-        if (!__any(have_pixel || alive)) break;
+        if (!__any(have_pixel || alive)) {
+            if (EXACT) while (dleft != 0u) drain_step(dleft);
+            break;
+        }
 
+        SEC_MARK(5);
+#if RT_SECTIONS
+        SEC_COUNT(0, 1);
+        SEC_COUNT(1, __popcll(__ballot(in_path)));
+        SEC_COUNT(2, __popcll(__ballot(dbg_vertex)));
+        SEC_COUNT(3, __popcll(__ballot(dbg_fin)));
+        SEC_COUNT(4, __popcll(__ballot(dbg_cam)));
+        dbg_vertex = dbg_fin = dbg_cam = false;
+#endif
         // ======================= trace both rays of every lane =======================
         const bool trA = in_path && hasA, trB = in_path && hasB;
         tA = 1.7976931348623157e308; triA = -1; occB = false;
         const bool fin = (!trA || finite3(rA)) && (!trB || finite3(rB)) && kargs4().force_walk == 0u;
         uint64_t ca = 0, cb = 0;
-        {
+        for (int rep = 0; rep < RT_REP_BOX; ++rep) {   // RT_REP_BOX > 1: cost-attribution builds only
+            if (RT_REP_BOX > 1) { ca = cb = 0; asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z)); }
             cfloat* bx = (cfloat*)kargs4().lboxes;
             const uint32_t nb = kargs4().n_lboxes;
             for (uint32_t b = 0; b < nb; ++b) {
@@ -375,6 +528,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                 if (box_hit(s0, s1, rA)) ca |= m;
                 if (box_hit(s0, s1, rB)) cb |= m;
             }
+            if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb));
         }
         if (!trA || !fin) ca = 0;
         if (!trB || !fin) cb = 0;
@@ -393,33 +547,63 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_coherent_kernel(KParams 
                 traverse_impl<false, false>(S, r, true, (double)slen, db, dt, occB, nt, tt);
             }
         }
+        SEC_MARK(6);
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
-        while ((ca | cb) != 0) {
-            const bool useA = ca != 0;
-            const uint64_t cur = useA ? ca : cb;
-            const int tri = __builtin_ctzll(cur);
-            if (useA) ca = cur & (cur - 1);
-            else cb = cur & (cur - 1);
-            const V3 d = useA ? dA : dB;
-            const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
-            double t;
-            if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
-                if (useA) {
-                    if (t <= tA) { tA = t; triA = tri; }
-                } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                    occB = true;
-                    cb = 0;
+        auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
+            while ((ca | cb) != 0) {
+#if RT_SECTIONS
+                SEC_COUNT(6, __popcll(__ballot(1)));
+                if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(5, 1);
+#endif
+                const bool useA = ca != 0;
+                const uint64_t cur = useA ? ca : cb;
+                const int tri = __builtin_ctzll(cur);
+                if (useA) ca = cur & (cur - 1);
+                else cb = cur & (cur - 1);
+                const V3 d = useA ? dA : dB;
+                const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
+                double t;
+                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                    if (useA) {
+                        if (t <= tA) { tA = t; triA = tri; }
+                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                        occB = true;
+                        cb = 0;
+                    }
                 }
             }
+        };
+        for (int rep = 1; rep < RT_REP_MT; ++rep) {   // cost-attribution builds only: results discarded
+            uint64_t xa = ca, xb = cb;
+            double xt = tA; int xtri = triA; bool xo = occB;
+            asm volatile("" : "+v"(xa), "+v"(xb), "+v"(o.x));
+            mt_loop(xa, xb, xt, xtri, xo);
+            asm volatile("" : : "v"(xt), "v"(xtri), "v"(xo));
         }
+        mt_loop(ca, cb, tA, triA, occB);
+        SEC_MARK(7);
     }
+#if RT_SECTIONS
+    // wave cycles per section -> counters[16 + section] (one atomic per wave and section)
+    if (__lane_id() == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long*)&P.counters[16 + i], (unsigned long long)sec_cyc[i]);
+    // wave-level counts live in the lane that counted them: reduce over the wave
+    for (int i = 0; i < 8; ++i) {
+        uint64_t v = sec_n[i];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+        if (__lane_id() == 0) atomicAdd((unsigned long long*)&P.counters[24 + i], (unsigned long long)v);
+    }
+#endif
 }
 
 template __global__ void pt_coherent_kernel<true>(KParams);
 template __global__ void pt_coherent_kernel<false>(KParams);
 
-size_t rt_coherent_lane_state_lds_bytes(bool exact) { return (size_t)(exact ? VS_WORDS_EXACT : VS_WORDS_FAST) * 256 * sizeof(float); }
+size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit)
+{
+    return (size_t)(lit ? (exact ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
+}
 
 hipError_t rt_launch_coherent(const KParams& P, bool exact, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
 {

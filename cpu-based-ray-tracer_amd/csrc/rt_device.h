@@ -26,14 +26,40 @@ __device__ __forceinline__ V3 neg(V3 a) { return V3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ float dot(V3 a, V3 b) { float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return (tx + ty) + tz; }
 // glm::cross, GLM/detail/func_geometric.inl:68-80
 __device__ __forceinline__ V3 cross(V3 x, V3 y) { return V3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+// ------------------------------------------------------------------------------ short reciprocals
+// 1 / (double)x for a finite nonzero float x, bit-identical to the IEEE double division: v_rcp_f64 and
+// two Newton steps.  The result depends only on x's 24-bit significand and exponent; every finite
+// nonzero float was checked exhaustively on gfx950 (tools/verify_rcp.hip).
+__device__ __forceinline__ double rcp_f64_of_f32(float x)
+{
+    const double b = (double)x;
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+// 1.0f / x, bit-identical to the correctly rounded division for every float x: v_rcp_f32 and one
+// Newton step where operand and result are normal (|x| in [2^-126, 2^126)), the division elsewhere
+// (exhaustive check as above)
+__device__ __forceinline__ float rcp_f32(float x)
+{
+    const float ax = __builtin_fabsf(x);
+    if (ax >= 0x1p-126f && ax < 0x1p126f) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    }
+    return 1.0f / x;
+}
+
 // glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
-__device__ __forceinline__ V3 glm_normalize(V3 v) { float is = 1.0f / __builtin_sqrtf(dot(v, v)); return muls(v, is); }
+__device__ __forceinline__ V3 glm_normalize(V3 v) { float is = rcp_f32(__builtin_sqrtf(dot(v, v))); return muls(v, is); }
 __device__ __forceinline__ float glm_length(V3 v) { return __builtin_sqrtf(dot(v, v)); }
 // Whitted::normalize (zero-safe), MC/VectorFloat.h:22-31
 __device__ __forceinline__ V3 w_normalize(V3 v)
 {
     float l2 = ((v.x * v.x) + (v.y * v.y)) + (v.z * v.z);
-    if (l2 > 0.0f) { float inv = 1.0f / __builtin_sqrtf(l2); return V3{v.x * inv, v.y * inv, v.z * inv}; }
+    if (l2 > 0.0f) { float inv = rcp_f32(__builtin_sqrtf(l2)); return V3{v.x * inv, v.y * inv, v.z * inv}; }
     return v;
 }
 // std::max / std::min / glm::max / glm::min: compare-select, the first operand survives a NaN
@@ -98,7 +124,7 @@ __device__ __forceinline__ Ray make_ray(V3 o, V3 d)
 {
     Ray r;
     r.o = o; r.d = d;
-    r.rcp = V3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    r.rcp = V3{rcp_f32(d.x), rcp_f32(d.y), rcp_f32(d.z)};
     r.nx = d.x < 0.0f; r.ny = d.y < 0.0f; r.nz = d.z < 0.0f;
     return r;
 }
@@ -151,12 +177,15 @@ __device__ __forceinline__ bool moller_trumbore_od(const V3& a, const V3& e1, co
     const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
     if (!(pos || ngt)) return false;
     if ((__builtin_fabsf(b2n) + __builtin_fabsf(b3n)) > __builtin_fabsf(den) * 1.00001f) return false;
-    const double inv = 1.0 / (double)den;
+    const double inv = rcp_f64_of_f32(den);   // == 1.0 / (double)den
     const double t = (double)tn * inv;
     const double b2 = (double)b2n * inv;
     const double b3 = (double)b3n * inv;
     t_out = t;
-    return (t > 0.0) && (b2 > 0.0) && (b3 > 0.0) && (((1.0 - b2) - b3) > 0.0);
+    // b2 > 0 and b3 > 0 follow from t > 0: tn, b2n, b3n share one strict sign (above), inv is finite
+    // and nonzero or NaN (den = +-inf: NaN, t > 0 fails as the reference's t = +-0 does), and no product
+    // of a nonzero float with inv underflows or overflows in double
+    return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
 }
 __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
 {

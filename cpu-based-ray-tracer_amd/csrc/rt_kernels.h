@@ -32,6 +32,7 @@ struct KParams {
     // frame-major: [frame - chunk_frames][local]) for the in-order sum of finalize_chunks_kernel
     uint32_t n_chunks, chunk_frames, items_per_chunk;
     float* lbuf; size_t lbuf_stride;
+    uint32_t park_all;              // every frame is parked (the vertex kernel): finalize accumulates all of them
     // outputs (compact local pixel order: local_row * W + x)
     float4* accum; uint32_t* rgba;
     // scratch
@@ -59,7 +60,7 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
 // (rt_coherent.hip); same KParams and LDS layout (scene | fold stack | lane state)
 hipError_t rt_launch_coherent(const KParams& P, bool exact, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
 int rt_coherent_occupancy(bool exact, int block, size_t lds_bytes);
-size_t rt_coherent_lane_state_lds_bytes(bool exact);
+size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 // Whitted Style Ray Tracer world (spheres + textured meshes, reflection/refraction recursion), config C1

@@ -603,8 +603,10 @@ __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_px) return;
-    float4 acc = P.accum[i];
-    const uint32_t nfp = P.n_frames - P.chunk_frames;
+    // park_all: every frame of the launch is parked, the accumulation starts from 0 at frame 1 and from
+    // the accumulator otherwise; else chunk 0 has accumulated in place and the later chunks are parked
+    float4 acc = (P.park_all && P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[i];
+    const uint32_t nfp = P.park_all ? P.n_frames : P.n_frames - P.chunk_frames;
     for (uint32_t b = 0; b * 4u < nfp; ++b) {
         const float4* blk = reinterpret_cast<const float4*>(P.lbuf + ((size_t)b * P.lbuf_stride + i) * 12u);
         const float4 q0 = blk[0], q1 = blk[1], q2 = blk[2];
@@ -627,7 +629,7 @@ __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_
 
 hipError_t rt_launch_finalize_chunks(const KParams& P, uint32_t n_px, hipStream_t stream)
 {
-    if (n_px == 0 || P.n_chunks <= 1) return hipSuccess;
+    if (n_px == 0 || (P.n_chunks <= 1 && !P.park_all)) return hipSuccess;
     hipLaunchKernelGGL(finalize_chunks_kernel, dim3((n_px + 255) / 256), dim3(256), 0, stream, P, n_px);
     return hipGetLastError();
 }
@@ -665,10 +667,10 @@ __global__ void math_kernel(uint32_t n, const float* __restrict__ x, float* __re
     if (i >= n) return;
     const float v = x[i];
     out[7 * i + 0] = __builtin_sqrtf(v);
-    out[7 * i + 1] = 1.0f / v;
+    out[7 * i + 1] = rcp_f32(v);   // the kernels' reciprocal (rt_device.h); == 1.0f / v correctly rounded
     out[7 * i + 2] = cos_f(v);
     out[7 * i + 3] = sin_f(v);
-    const double r = 1.0 / (double)v;
+    const double r = rcp_f64_of_f32(v);   // Moller-Trumbore's 1 / (double)den (rt_device.h)
     out[7 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
     out[7 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));
     out[7 * i + 6] = pow_lobe(v, 25.0f);   // the C1 specular lobe, powf(x, specular_size_factor = 25)

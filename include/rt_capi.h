@@ -191,6 +191,9 @@ typedef struct {
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */
 #define RT_KERNEL_WHITTED 2   /* whitted_kernel / whitted_world_kernel (rt_whitted.hip) */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
+/* diagnostic: the raw device counters of the last rt_render (32 x u64; [16..23] = wave cycles per
+ * section of the vertex kernel in RT_SECTIONS builds), after a stream synchronisation */
+rt_status rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* ------------------------------------------------------------------ the Denoiser (DN/ = Denoiser/8599RayTracerGUI/src/)
  * One call = one Renderer::Render of the Denoiser project (DN/Renderer.cpp:101-283): a 1-spp path-traced

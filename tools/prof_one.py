@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""One warm-up + one measured C4-shaped render with a given library build, for rocprofv3 PMC passes
+comparing builds (profiles/run_rocprof.sh profiles bench.py itself).
+
+    rocprofv3 --pmc SQ_INSTS_VALU -- python3 tools/prof_one.py librt_hip.so --spp 64
+"""
+import argparse
+import importlib.util
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib")
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--fast", action="store_true")
+    ap.add_argument("--sections", action="store_true", help="print the wave-cycle split of an RT_SECTIONS build")
+    args = ap.parse_args()
+    spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(PKG, "__init__.py"))
+    rt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(rt)
+    rt.LIB_PATH = os.path.join(PKG, args.lib)
+    c = rt.Context(0)
+    c.upload(rt.Scene.cornell())
+    c.resize(args.width, args.height)
+    cam, _, _ = rt.camera_default(args.width, args.height)
+    for _ in range(2):
+        c.render(cam, args.spp, fetch=False, exact=not args.fast)
+    st = c.stats()
+    print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
+    if args.sections:
+        cyc = c.debug_counters(24)[16:24]
+        names = ["service head", "vertex", "finish", "queue", "camera", "box loop", "moller-trumbore", "(entry)"]
+        tot = float(sum(cyc)) or 1.0
+        print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
+        n = c.debug_counters(32)[24:32]
+        it = max(n[0], 1)
+        print({"wave_iterations": n[0], "lanes_on_path/it": round(n[1] / it, 2), "vertex/it": round(n[2] / it, 2),
+               "finish/it": round(n[3] / it, 2), "camera/it": round(n[4] / it, 2), "mt_iters/it": round(n[5] / it, 2),
+               "mt_lane_util": round(n[6] / max(n[5], 1) / 64, 3), "fold_iters/it": round(n[7] / it, 2),
+               "iterations_per_sample_lane": round(n[0] * 64 / (args.width * args.height * args.spp), 3)})
+    c.close()
+
+
+if __name__ == "__main__":
+    main()
