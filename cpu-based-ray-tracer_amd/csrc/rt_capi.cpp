@@ -494,6 +494,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         return coh ? rt_coherent_occupancy(exact, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };
     const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0) : rt_lane_state_lds_bytes(exact);
+    if (coh) {   // the vertex kernel reads the leaf boxes with scalar loads: they are not staged in LDS
+        P.lds_scene_quads -= 2 * P.n_lboxes;
+    }
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
@@ -504,7 +507,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             if (occupancy(used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
-    const size_t shmem = (lds ? lds_bytes : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
+    const size_t shmem = (lds ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;

@@ -35,18 +35,18 @@ namespace {
 
 // per-lane cold state in LDS, [field][lane] words
 enum : uint32_t {
-    VS_LOCAL = 0, VS_XY = 1, VS_C = 2,   // the work item: local pixel, (x, y) global, frame chunk
-    VS_PIX = 3, VS_FRAME = 4,            // the sample's stream counter (pixel, frame)
-    VS_LD = 5,                           // the pending vertex's unoccluded direct term (3 words)
-    VS_PCOS = 8, VS_MAT = 9,             // the pending vertex's indirect cosine and material
-    VS_BASE = 10,                        // EXACT: ring position of the current path's level 0
-    VS_DL = 11,                          // EXACT drain: the partial fold (3 words)
-    VS_DPOS = 14,                        // EXACT drain: ring position of the next level to fold
-    VS_DT0 = 15, VS_DT1 = 16,            // EXACT drain: the sample's local pixel and frame index
-    VS_THR = 10, VS_LSUM = 13,           // FAST: throughput, radiance
-    VS_WORDS_EXACT = 17, VS_WORDS_FAST = 16,
-    VS_RNG = 17,                         // unlit scenes only: the Philox block of the current 4 draws
-    VS_WORDS_UNLIT = 21
+    VS_LOCAL = 0,                        // the work item's local pixel
+    VS_PIX = 1, VS_FRAME = 2,            // the sample's stream counter: global pixel y * W + x, frame number
+    VS_LD = 3,                           // the pending vertex's unoccluded direct term (3 words)
+    VS_PCOS = 6, VS_MAT = 7,             // the pending vertex's indirect cosine and material
+    VS_BASE = 8,                         // EXACT: ring position of the current path's level 0
+    VS_DL = 9,                           // EXACT drain: the partial fold (3 words)
+    VS_DPOS = 12,                        // EXACT drain: ring position of the next level to fold
+    VS_DT0 = 13, VS_DT1 = 14,            // EXACT drain: the sample's local pixel and frame index
+    VS_THR = 8, VS_LSUM = 11,            // FAST: throughput, radiance
+    VS_WORDS_EXACT = 15, VS_WORDS_FAST = 14,
+    VS_RNG = 15,                         // unlit scenes only: the Philox block of the current 4 draws
+    VS_WORDS_UNLIT = 19
 };
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
@@ -98,7 +98,6 @@ struct VertexRng {
     // whose vertices draw through next())
     __device__ __forceinline__ void camera_draws(uint32_t px, uint32_t fr, bool keep, float& ux, float& uy)
     {
-        w[VS_PIX * 256u] = px; w[VS_FRAME * 256u] = fr;
         uint32_t o[4];
         philox4x32_10(px, fr, 0u, 0u, k0, k1, o);
         if (keep) { w[VS_RNG * 256u] = o[0]; w[(VS_RNG + 1) * 256u] = o[1]; w[(VS_RNG + 2) * 256u] = o[2]; w[(VS_RNG + 3) * 256u] = o[3]; }
@@ -131,9 +130,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 
 }  // namespace
 
-// minimum waves per SIMD the register allocation must admit: 7 (72 VGPRs) fits without spilling VGPRs
+// minimum waves per SIMD the register allocation must admit: 8 = at most 64 VGPRs (no VGPR spill; a
+// few SGPRs spill to VGPR lanes) and 78 SGPRs, so 8 blocks of 256 lanes are resident per CU -- the
+// hardware admits min(8, 800 / (ceil(sgpr / 16) * 16 + 16)) blocks (MI355X_MICROARCH.md, Residency),
+// one fewer than the occupancy API at 82-96 SGPRs -- with 15 LDS words per lane (+1-2 % over 7)
 #ifndef RT_COH_MIN_WAVES
-#define RT_COH_MIN_WAVES 7
+#define RT_COH_MIN_WAVES 8
 #endif
 // cost attribution (A/B builds, tools/ab_libs.py): run the leaf-box loop / the Moller-Trumbore loop
 // this many times per trace step (extra runs' results are discarded; the image is unchanged)
@@ -159,7 +161,8 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
     SceneView S;
     S.n_nodes = P.n_nodes;
     {
-        // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris | lboxes)
+        // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris; the leaf boxes
+        // are read with scalar loads)
         const uint32_t nq = 2 * P.n_nodes, tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
         float4* dn = lds_scene;
         float4* dt = dn + nq;
@@ -298,8 +301,8 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
                         const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
                         const uint32_t local = lr * Q.W + lx;
                         lsu(VS_LOCAL) = local;
-                        lsu(VS_XY) = lx | (y << 16);
-                        lsu(VS_C) = c;
+                        lsu(VS_PIX) = y * Q.W + lx;
+                        lsu(VS_FRAME) = Q.first_frame + c * Q.chunk_frames;   // the frame of the item's first sample
                         have_pixel = true;
                         k = 0;
                     }
@@ -435,9 +438,11 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
             if (finished) {
                 in_path = false;
                 hasA = hasB = false;
-                const uint32_t local = lsu(VS_LOCAL), kbase = lsu(VS_C) * Q.chunk_frames;
-                const uint32_t fidx = kbase + k;   // the sample's frame index in this launch
+                const uint32_t local = lsu(VS_LOCAL), frame = lsu(VS_FRAME);
+                const uint32_t fidx = frame - Q.first_frame;   // the sample's frame index in this launch
+                const uint32_t kbase = fidx - k;               // the item's first frame index
                 ++k;
+                lsu(VS_FRAME) = frame + 1u;
                 const bool last = k == min(Q.chunk_frames, Q.n_frames - kbase);
                 if (last) have_pixel = false;
                 if (EXACT) {
@@ -473,9 +478,9 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
             CKParams& Q = kargs4();
-            const uint32_t xy = lsu(VS_XY), x = xy & 0xFFFFu, y = xy >> 16;
+            const uint32_t pix = lsu(VS_PIX), y = pix / Q.W, x = pix - y * Q.W;
             float ux, uy;
-            g.camera_draws(y * Q.W + x, Q.first_frame + lsu(VS_C) * Q.chunk_frames + k, !Q.has_light, ux, uy);
+            g.camera_draws(pix, lsu(VS_FRAME), !Q.has_light, ux, uy);
 #if RT_SECTIONS
             dbg_cam = true;
 #endif
