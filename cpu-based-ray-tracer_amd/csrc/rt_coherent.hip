@@ -137,6 +137,11 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_COH_MIN_WAVES
 #define RT_COH_MIN_WAVES 8
 #endif
+// work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
+// more than one item per lane, so the launch tail stays one item long)
+#ifndef WQ_BATCH
+#define WQ_BATCH 64u
+#endif
 // cost attribution (A/B builds, tools/ab_libs.py): run the leaf-box loop / the Moller-Trumbore loop
 // this many times per trace step (extra runs' results are discarded; the image is unchanged)
 #ifndef RT_REP_BOX
@@ -242,6 +247,7 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
     // ends while the previous fold still drains first completes that fold, so the per-pixel order of the
     // accumulation is the frame order.
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
+    uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     if (EXACT) lsu(VS_BASE) = 0u;
 
 #if RT_SECTIONS
@@ -276,17 +282,25 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
         }
         // ======================= lane-level work queue (wave-collective) =======================
         // at the top of the iteration, before any store: a lane that finished its item in the previous
-        // iteration takes the next one (the returning atomic waits for no store of this iteration)
+        // iteration takes the next one (the returning atomic waits for no store of this iteration).
+        // The wave takes items from the device counter in batches of WQ_BATCH into a wave-private pool
+        // (two uniform registers); lanes are served from the pool in lane order.  One returning atomic
+        // on one word saturates near 88 dequeues/us (MI355X_MICROARCH.md, dequeue): one per refill
+        // (a lane or two per wave and iteration) was the limit at 16-frame chunks.
         const bool need = alive && !have_pixel;
         const uint64_t mask = __ballot(need);
         if (mask != 0) {
             CKParams& Q = kargs4();
-            uint32_t base = 0;
-            const int leader = __ffsll((unsigned long long)mask) - 1;
-            if ((int)lane == leader) base = atomicAdd(Q.work_counter, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
+            const uint32_t n = (uint32_t)__popcll(mask);
+            uint32_t fresh = 0;   // first item of a new batch (wave-uniform)
+            if (n > pool_count) {
+                uint32_t b = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, WQ_BATCH);
+                fresh = __builtin_amdgcn_readfirstlane(b);
+            }
             if (need) {
-                const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t w = j < pool_count ? pool_base + j : fresh + (j - pool_count);
                 if (w >= Q.n_items) {
                     alive = false;
                 } else {
@@ -307,6 +321,13 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
                         k = 0;
                     }
                 }
+            }
+            if (n > pool_count) {
+                pool_base = fresh + (n - pool_count);
+                pool_count = WQ_BATCH - (n - pool_count);
+            } else {
+                pool_base += n;
+                pool_count -= n;
             }
         }
 
