@@ -1,9 +1,9 @@
 // rt_kernels.hip -- the MI355X path-tracing megakernel (gfx950 / CDNA4, wave64).
 //
 // One persistent launch renders `n_frames` samples of every pixel assigned to this device:
-//   * lane-level work queue: a lane that finishes all frames of its pixel fetches the next pixel
-//     from a device atomic (one atomic per wave per refill: __ballot + mbcnt compaction), so the
-//     wave stays full until the queue drains; pixel order is 8x8-tile swizzled for ray coherence;
+//   * lane-level work queue: a lane that finishes its work item takes the next one from its wave's
+//     pool (__ballot + popcount compaction), which refills 64 items per device atomic, so the wave
+//     stays full until the queue drains; pixel order is 8x8-tile swizzled for ray coherence;
 //   * per-pixel frames run in order inside the lane (accum += L per frame exactly like
 //     Renderer::RayGen_Shader, MC/Renderer.cpp:124-134), so the float accumulation is the
 //     reference's, bit for bit;
@@ -46,6 +46,9 @@ enum : uint32_t {
 
 }  // namespace
 
+#ifndef WQ_BATCH
+#define WQ_BATCH 64u     // work items per refill of a wave's pool (<= 64: at most one per lane)
+#endif
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1   // minimum waves per SIMD the register allocation must admit (A/B knob)
 #endif
@@ -123,6 +126,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
     bool tdone = true;
 
     uint64_t c_service = 0, c_queue = 0, c_trace = 0, s_lanes = 0;   // COUNT: wave-uniform cycle sums
+    uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     for (;;) {
         // ======================= service round: lanes whose ray has been traced =======================
         uint64_t tc0 = 0;
@@ -328,16 +332,25 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
         uint64_t tc1 = 0;
         if (COUNT) { tc1 = clock64(); c_service += tc1 - tc0; }
         // ======================= lane-level work queue (wave-collective) =======================
+        // items come from a wave-private pool refilled WQ_BATCH at a time from the device counter
+        // (one returning atomic per refill saturates a single counter word: rt_coherent.hip)
         const bool need = alive && !have_pixel;
         const uint64_t mask = __ballot(need);
         if (mask != 0) {
             const KParams& Q = kargs();
-            uint32_t base = 0;
-            const int leader = __ffsll((unsigned long long)mask) - 1;
-            if ((int)lane == leader) base = atomicAdd(Q.work_counter, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
+            const uint32_t n = (uint32_t)__popcll(mask);
+            uint32_t fresh = 0;
+            if (n > pool_count) {
+                uint32_t b = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, WQ_BATCH);
+                fresh = __builtin_amdgcn_readfirstlane(b);
+            }
+            const uint32_t pb = pool_base, pc = pool_count;
+            if (n > pc) { pool_base = fresh + (n - pc); pool_count = WQ_BATCH - (n - pc); }
+            else { pool_base = pb + n; pool_count = pc - n; }
             if (need) {
-                const uint32_t w = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t w = j < pc ? pb + j : fresh + (j - pc);
                 if (w >= Q.n_items) {
                     alive = false;
                 } else {
