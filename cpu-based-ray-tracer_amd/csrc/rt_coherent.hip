@@ -158,6 +158,16 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_PAD_VALU
 #define RT_PAD_VALU 0
 #endif
+// leaf boxes per group in the box loop: one scalar-load wait per 2 boxes (s_load_dwordx16) instead of
+// one per box; +0.9 % C4 over 1 (tools/ab_libs.py; 2: +0.6 %)
+#ifndef RT_BOX_UNROLL
+#define RT_BOX_UNROLL 4
+#endif
+// Moller-Trumbore loop: load the next candidate's triangle before testing the current one (A/B knob;
+// as written 14 VGPRs spill at 8 waves per SIMD: -6 %)
+#ifndef RT_MT_PREFETCH
+#define RT_MT_PREFETCH 0
+#endif
 
 template <bool EXACT>
 __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
@@ -547,13 +557,22 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
             if (RT_REP_BOX > 1) { ca = cb = 0; asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z)); }
             cfloat* bx = (cfloat*)kargs4().lboxes;
             const uint32_t nb = kargs4().n_lboxes;
-            for (uint32_t b = 0; b < nb; ++b) {
-                cfloat* q = bx + 8 * b;   // (lo.xyz, mask 0-31)(hi.xyz, mask 32-63), rt_layout.h
+            auto one_box = [&](cfloat* q) {   // (lo.xyz, mask 0-31)(hi.xyz, mask 32-63), rt_layout.h
                 const V3 s0{q[0] - o.x, q[1] - o.y, q[2] - o.z}, s1{q[4] - o.x, q[5] - o.y, q[6] - o.z};
                 const uint64_t m = (uint64_t)(uint32_t)f2i(q[3]) | ((uint64_t)(uint32_t)f2i(q[7]) << 32);
                 if (box_hit(s0, s1, rA)) ca |= m;
                 if (box_hit(s0, s1, rB)) cb |= m;
+            };
+            uint32_t b = 0;
+#if RT_BOX_UNROLL > 1
+            // RT_BOX_UNROLL boxes per scalar load (one wait per group instead of one per box)
+            for (; b + RT_BOX_UNROLL <= nb; b += RT_BOX_UNROLL) {
+                cfloat* q = bx + 8 * b;
+#pragma unroll
+                for (int u = 0; u < RT_BOX_UNROLL; ++u) one_box(q + 8 * u);
             }
+#endif
+            for (; b < nb; ++b) one_box(bx + 8 * b);
             if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb));
         }
         if (!trA || !fin) ca = 0;
@@ -577,6 +596,40 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
         auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
+#if RT_MT_PREFETCH
+            // the next candidate's vertices are read from LDS before the current candidate is tested
+            auto take = [&](bool& useA) -> int {
+                useA = ca != 0;
+                const uint64_t cur = useA ? ca : cb;
+                if (useA) ca = cur & (cur - 1);
+                else cb = cur & (cur - 1);
+                return cur != 0 ? __builtin_ctzll(cur) : -1;
+            };
+            auto fetch = [&](int tri, V3& a, V3& e1, V3& e2) {
+                const float4* q = S.tris + 4 * (tri < 0 ? 0 : tri);
+                a = V3{q[0].x, q[0].y, q[0].z}; e1 = V3{q[1].x, q[1].y, q[1].z}; e2 = V3{q[2].x, q[2].y, q[2].z};
+            };
+            bool useA;
+            int tri = take(useA);
+            V3 a, e1, e2;
+            fetch(tri, a, e1, e2);
+            while (tri >= 0) {
+                bool nuse;
+                const int nt = take(nuse);
+                V3 na, ne1, ne2;
+                fetch(nt, na, ne1, ne2);
+                double t;
+                if (moller_trumbore_od(a, e1, e2, o, useA ? dA : dB, t)) {
+                    if (useA) {
+                        if (t <= tA) { tA = t; triA = tri; }
+                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                        occB = true;
+                        break;   // B's candidates come last: nothing else to test
+                    }
+                }
+                tri = nt; useA = nuse; a = na; e1 = ne1; e2 = ne2;
+            }
+#else
             while ((ca | cb) != 0) {
 #if RT_SECTIONS
                 SEC_COUNT(6, __popcll(__ballot(1)));
@@ -599,6 +652,7 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
                     }
                 }
             }
+#endif
         };
         for (int rep = 1; rep < RT_REP_MT; ++rep) {   // cost-attribution builds only: results discarded
             uint64_t xa = ca, xb = cb;
