@@ -53,7 +53,7 @@ class Stats(C.Structure):
 
 _DIAGNOSTIC = {"rt_debug_counters"}
 
-KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel"}
+KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 
 
 class DenoiseParams(C.Structure):

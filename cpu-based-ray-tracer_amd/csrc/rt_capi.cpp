@@ -68,8 +68,10 @@ struct rt_ctx {
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
+    bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
+    uint32_t vthresh = 40, vsteps = 8; // the same for the vertex kernel's BVH variant (C5 sweep)
 };
 
 namespace {
@@ -316,11 +318,12 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     rt_ctx* c = new (std::nothrow) rt_ctx;
     if (!c) return RT_ERR_OOM;
     c->device = cfg ? cfg->device : 0;
-    if (const char* e = std::getenv("RT_THRESH")) c->thresh = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_STEPS")) c->steps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = std::getenv("RT_THRESH")) c->thresh = c->vthresh = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_STEPS")) c->steps = c->vsteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -358,7 +361,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
             c->occ_global[ex][cn] = b > 0 ? b : 2;
             if (ex) ex_max = std::max(ex_max, c->occ_global[ex][cn]);
         }
-    ex_max = std::max(ex_max, rt_coherent_occupancy(true, 256, 0));
+    ex_max = std::max({ex_max, rt_coherent_occupancy(true, false, 256, 0), rt_coherent_occupancy(true, true, 256, 0)});
     c->block = 256;
     // the EXACT fold stack is sized for the largest grid any mode launches (LDS staging never
     // raises occupancy above the register-limited value)
@@ -489,13 +492,20 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const bool lds = (p->flags & RT_RENDER_GLOBAL_SCENE) == 0 && lds_bytes <= kMaxLdsScene;
     P.lds_scene_quads = lds ? (uint32_t)(lds_bytes / sizeof(float4)) : 0;
     // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
-    const bool coh = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
+    // any other path scene: its BVH variant, the scene in HBM (RT_VERTEX_BVH=0: the megakernel)
+    const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
+    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted;
+    const bool coh = coh_box || coh_bvh;
     auto occupancy = [&](size_t bytes) {
-        return coh ? rt_coherent_occupancy(exact, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
+        return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };
     const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0) : rt_lane_state_lds_bytes(exact);
-    if (coh) {   // the vertex kernel reads the leaf boxes with scalar loads: they are not staged in LDS
+    if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads: they are not staged in LDS
         P.lds_scene_quads -= 2 * P.n_lboxes;
+    }
+    if (coh_bvh) {   // the BVH variant reads the scene from HBM
+        P.lds_scene_quads = 0;
+        P.thresh = c->vthresh; P.steps = c->vsteps;
     }
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
@@ -507,7 +517,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             if (occupancy(used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
-    const size_t shmem = (lds ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
+    const size_t shmem = (lds && !coh_bvh ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
@@ -572,7 +582,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local;
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
-                if (coh) HIPC(c, rt_launch_coherent(Q, exact, grid, c->block, shmem, c->stream));
+                if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
                 HIPC(c, rt_launch_finalize_chunks(Q, (uint32_t)px_local, c->stream));
                 c->stats.n_chunks = n_chunks;
@@ -581,7 +591,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             c->stats.n_passes = passes;
         }
         c->stats.grid = grid;
-        c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);
+        c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh_bvh ? RT_KERNEL_VERTEX_BVH : coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);
         HIPC(c, hipEventRecord(c->ev1, c->stream));
         c->pending_stats = true;
     }

@@ -169,13 +169,27 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #define RT_MT_PREFETCH 0
 #endif
 
-template <bool EXACT>
-__global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
+// the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
+#ifndef RT_COH_BVH_MIN_WAVES
+#define RT_COH_BVH_MIN_WAVES 8
+#endif
+
+struct FiniteSlab { static constexpr bool value = true; };
+struct GeneralSlab { static constexpr bool value = false; };
+
+// BVH = false: the scene in LDS, both rays against the distinct leaf boxes (one wave-uniform loop).
+// BVH = true: the scene in HBM (read through L2/MALL); the two rays of a lane walk the stackless BVH
+// one after the other (A, then B) in the megakernel's rounds of `steps` box tests with up to two
+// postponed leaves, and a lane is served once both of its rays are done.
+template <bool EXACT, bool BVH>
+__global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
     SceneView S;
     S.n_nodes = P.n_nodes;
-    {
+    if (BVH) {
+        S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = nullptr;
+    } else {
         // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris; the leaf boxes
         // are read with scalar loads)
         const uint32_t nq = 2 * P.n_nodes, tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
@@ -259,6 +273,9 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
     uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     if (EXACT) lsu(VS_BASE) = 0u;
+    // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
+    const uint32_t NN = S.n_nodes;
+    uint32_t tiA = NN, tiB = NN;
 
 #if RT_SECTIONS
     uint64_t sec_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -342,7 +359,8 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
         }
 
         // ======================= service: every lane on a path has its rays back =======================
-        if (in_path) {
+        // (BVH: the lanes whose two rays are done)
+        if (in_path && (!BVH || (tiA >= NN && tiB >= NN))) {
             CKParams& Q = kargs4();
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
@@ -463,6 +481,10 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
                 o = p;
                 pend = true;
                 depth = depth + 1;
+                if (BVH) {
+                    tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
+                    tA = 1.7976931348623157e308; triA = -1; occB = false;
+                }
             }
 
             SEC_MARK(2);
@@ -531,6 +553,10 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
             depth = 0;
             pend = false;
             in_path = true;
+            if (BVH) {
+                tiA = 0u; tiB = NN;
+                tA = 1.7976931348623157e308; triA = -1; occB = false;
+            }
             if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
         }
 
@@ -549,6 +575,7 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
         dbg_vertex = dbg_fin = dbg_cam = false;
 #endif
         // ======================= trace both rays of every lane =======================
+        if (!BVH) {
         const bool trA = in_path && hasA, trB = in_path && hasB;
         tA = 1.7976931348623157e308; triA = -1; occB = false;
         const bool fin = (!trA || finite3(rA)) && (!trB || finite3(rB)) && kargs4().force_walk == 0u;
@@ -662,6 +689,61 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
             asm volatile("" : : "v"(xt), "v"(xtri), "v"(xo));
         }
         mt_loop(ca, cb, tA, triA, occB);
+        } else {
+            // BVH rounds (the megakernel's, rt_kernels.hip): `steps` box tests per round on the lane's
+            // current ray (A until it is done, then B), up to two leaves postponed in DFS order and
+            // intersected at the end of the round.  Rounds continue while more than `thresh` lanes
+            // trace or nobody waits for service.
+            CKParams& Q = kargs4();
+            const uint32_t thresh = Q.thresh, steps = Q.steps;
+            for (;;) {
+                const bool tracing = in_path && (tiA < NN || tiB < NN);
+                const uint64_t act = __ballot(tracing);
+                if (act == 0) break;
+                const uint64_t srv = __ballot((in_path && !tracing) || (alive && !have_pixel));
+                if ((uint32_t)__popcll(act) <= thresh && srv != 0) break;
+                const bool curA = tiA < NN;
+                const V3 d = curA ? dA : dB;
+                const Ray r{o, d, curA ? rA : rB, d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
+                const bool fin = __all(!tracing || finite3(r.rcp));
+                if (tracing) {
+                    uint32_t ti = curA ? tiA : tiB;
+                    int parked0 = -1, parked1 = -1;
+                    auto walk = [&](auto kind) {
+                        for (uint32_t s = 0; s < steps && ti < NN; ++s) {
+                            const float4 q0 = S.nodes[2 * ti];
+                            const float4 q1 = S.nodes[2 * ti + 1];
+                            const bool hit = decltype(kind)::value ? slab_hit_finite(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y)
+                                                                   : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                            const int tri = f2i(q1.w);
+                            ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
+                            if (hit && tri >= 0) {
+                                if (parked0 < 0) parked0 = tri;
+                                else { parked1 = tri; break; }
+                            }
+                        }
+                    };
+                    if (fin) walk(FiniteSlab{});
+                    else walk(GeneralSlab{});
+                    for (int slot = 0; slot < 2; ++slot) {
+                        const int pk = slot == 0 ? parked0 : parked1;
+                        if (pk < 0 || (!curA && occB)) continue;
+                        const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
+                        double t;
+                        if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                            if (curA) {
+                                if (t <= tA) { tA = t; triA = pk; }   // the later leaf wins ties
+                            } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                                occB = true;
+                                ti = NN;
+                            }
+                        }
+                    }
+                    if (curA) tiA = ti;
+                    else tiB = ti;
+                }
+            }
+        }
         SEC_MARK(7);
     }
 #if RT_SECTIONS
@@ -677,25 +759,35 @@ __global__ void __launch_bounds__(256, RT_COH_MIN_WAVES) pt_coherent_kernel(KPar
 #endif
 }
 
-template __global__ void pt_coherent_kernel<true>(KParams);
-template __global__ void pt_coherent_kernel<false>(KParams);
+template __global__ void pt_coherent_kernel<true, false>(KParams);
+template __global__ void pt_coherent_kernel<false, false>(KParams);
+template __global__ void pt_coherent_kernel<true, true>(KParams);
+template __global__ void pt_coherent_kernel<false, true>(KParams);
 
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit)
 {
     return (size_t)(lit ? (exact ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
 }
 
-hipError_t rt_launch_coherent(const KParams& P, bool exact, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
+hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
 {
-    if (exact) hipLaunchKernelGGL(pt_coherent_kernel<true>, dim3(grid), dim3(block), lds, stream, P);
-    else hipLaunchKernelGGL(pt_coherent_kernel<false>, dim3(grid), dim3(block), lds, stream, P);
+    if (bvh) {
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, true>), dim3(grid), dim3(block), lds, stream, P);
+    } else {
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, false>), dim3(grid), dim3(block), lds, stream, P);
+    }
     return hipGetLastError();
 }
 
-int rt_coherent_occupancy(bool exact, int block, size_t lds_bytes)
+int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes)
 {
     int n = 0;
-    const hipError_t e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true>, block, lds_bytes)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false>, block, lds_bytes);
+    hipError_t e;
+    if (bvh) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true>, block, lds_bytes)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true>, block, lds_bytes);
+    else e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, false>, block, lds_bytes)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, false>, block, lds_bytes);
     return e == hipSuccess ? n : 0;
 }

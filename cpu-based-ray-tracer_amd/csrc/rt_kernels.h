@@ -56,10 +56,10 @@ size_t rt_stack_lds_bytes(uint32_t levels);
 size_t rt_lane_state_lds_bytes(bool exact);   // the megakernel's per-lane cold state (256 lanes)
 hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool lds, uint32_t grid, uint32_t block, hipStream_t stream);
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
-// small scenes (n_lboxes > 0, scene in LDS, no counters, no G-buffer): the vertex-synchronous kernel
-// (rt_coherent.hip); same KParams and LDS layout (scene | fold stack | lane state)
-hipError_t rt_launch_coherent(const KParams& P, bool exact, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
-int rt_coherent_occupancy(bool exact, int block, size_t lds_bytes);
+// the vertex-synchronous kernel (rt_coherent.hip; no counters, no G-buffer): small scenes (n_lboxes > 0,
+// scene in LDS: LDS = scene | lane state) or, bvh = true, any scene in HBM (LDS = lane state)
+hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
+int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes);
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);

@@ -190,6 +190,7 @@ typedef struct {
 #define RT_KERNEL_MEGA 0      /* pt_megakernel (rt_kernels.hip): any scene, counters, G-buffer frames */
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */
 #define RT_KERNEL_WHITTED 2   /* whitted_kernel / whitted_world_kernel (rt_whitted.hip) */
+#define RT_KERNEL_VERTEX_BVH 3   /* pt_coherent_kernel's BVH variant (rt_coherent.hip): other path scenes */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 /* diagnostic: the raw device counters of the last rt_render (32 x u64; [16..23] = wave cycles per
  * section of the vertex kernel in RT_SECTIONS builds), after a stream synchronisation */

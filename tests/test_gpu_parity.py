@@ -265,3 +265,37 @@ def test_vertex_kernel_equals_megakernel(monkeypatch, exact):
     for name in ("mega", "walk", "vertex_chunks"):
         assert np.array_equal(out[name][0], out["vertex"][0]), name
         assert np.array_equal(bits(out[name][1]), bits(out["vertex"][1])), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ["cornell_bvh", "c5"])
+@pytest.mark.parametrize("exact", [True, False])
+def test_vertex_bvh_kernel_equals_megakernel(monkeypatch, scene, exact):
+    """Scenes without decisive leaf boxes render with the vertex kernel's BVH variant (the scene in HBM,
+    two rays per lane walking the stackless BVH): the Cornell box with RT_BRUTE=0 and the C5 scene
+    (Cornell + 79k-triangle mesh).  RT_VERTEX_BVH=0 runs the megakernel; same bits, with and without
+    frame chunks."""
+    out = {}
+    for name, env in (("vertex", {}), ("mega", {"RT_VERTEX_BVH": "0"}), ("vertex_chunks", {"RT_CHUNKS": "3"})):
+        for k in ("RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_CHUNKS"):
+            monkeypatch.delenv(k, raising=False)
+        if scene == "cornell_bvh":
+            monkeypatch.setenv("RT_BRUTE", "0")
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = rt.Context(0)
+        try:
+            if scene == "c5":
+                c.upload(rt.Scene.cornell_c5(np.load(os.path.join(os.path.dirname(__file__), "golden", "bvh_scene.npz"))["raw_bunny"]))
+            else:
+                c.upload(rt.Scene.cornell())
+            c.resize(72, 48)
+            cam, _, _ = rt.camera_default(72, 48)
+            rgba, a = c.render(cam, 16, seed=7, exact=exact)
+            out[name] = (rgba, a, c.stats().kernel)
+        finally:
+            c.close()
+    assert out["vertex"][2] == 3 and out["mega"][2] == 0
+    for name in ("mega", "vertex_chunks"):
+        assert np.array_equal(out[name][0], out["vertex"][0]), name
+        assert np.array_equal(bits(out[name][1]), bits(out["vertex"][1])), name
