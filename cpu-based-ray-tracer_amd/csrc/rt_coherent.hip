@@ -168,6 +168,10 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_MT_PREFETCH
 #define RT_MT_PREFETCH 0
 #endif
+// ring levels loaded together when a fold is completed at once (drain_all; A/B knob)
+#ifndef RT_DRAIN_BATCH
+#define RT_DRAIN_BATCH 2
+#endif
 
 // the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
 #ifndef RT_COH_BVH_MIN_WAVES
@@ -247,6 +251,43 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             st3(VS_DL, L);
             lsu(VS_DPOS) = (pos == 0u ? Q.stack_depth : pos) - 1u;
         }
+    };
+    // the rest of a draining fold at once (a path ended while the previous one still drains): the ring
+    // loads of RT_DRAIN_BATCH levels are issued together, then folded in order, so the wave waits for
+    // one load latency per batch instead of one per level
+    auto drain_all = [&](uint32_t& dleft) {
+#if RT_DRAIN_BATCH > 1
+        if (dleft == 0u) return;
+        CKParams& Q = kargs4();
+        const uint32_t R = Q.stack_depth;
+        uint32_t pos = lsu(VS_DPOS);
+        V3 L = ls3(VS_DL);
+        while (dleft != 0u) {
+            float4 e[RT_DRAIN_BATCH];
+            int m[RT_DRAIN_BATCH];
+#pragma unroll
+            for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
+                const uint32_t pj = pos >= j ? pos - j : pos + R - j;
+                const uint32_t at = j < dleft ? pj : pos;   // levels past the fold re-read the first one (unused)
+                e[j] = Q.stack_ld[(size_t)at * Q.total_threads + gtid];
+                m[j] = Q.stack_mat[(size_t)at * Q.total_threads + gtid];
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
+                if (j < dleft) {
+                    const float4 mb2 = S.mats[2 * m[j]];
+                    const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
+                    L = add(V3{e[j].x, e[j].y, e[j].z}, divs(divs(muls(mul(L, f), e[j].w), PDF), Q.rr));
+                }
+            }
+            const uint32_t n = dleft < RT_DRAIN_BATCH ? dleft : RT_DRAIN_BATCH;
+            pos = pos >= n ? pos - n : pos + R - n;
+            dleft -= n;
+        }
+        complete(L, lsu(VS_DT0), lsu(VS_DT1));
+#else
+        while (dleft != 0u) drain_step(dleft);
+#endif
     };
 
     bool alive = true, have_pixel = false, in_path = false;
@@ -502,7 +543,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #if RT_SECTIONS
                     if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(7, 1);
 #endif
-                    while (dleft != 0u) drain_step(dleft);   // the previous sample's fold completes first
+                    drain_all(dleft);   // the previous sample's fold completes first
                     const uint32_t m = (uint32_t)(fold_top + 1);
                     const uint32_t base = lsu(VS_BASE);
                     if (m == 0u) {
@@ -561,7 +602,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         }
 
         if (!__any(have_pixel || alive)) {
-            if (EXACT) while (dleft != 0u) drain_step(dleft);
+            if (EXACT) drain_all(dleft);
             break;
         }
 
