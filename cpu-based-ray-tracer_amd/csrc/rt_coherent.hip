@@ -172,6 +172,11 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_DRAIN_BATCH
 #define RT_DRAIN_BATCH 2
 #endif
+// complete the previous fold at the top of the iteration when the path will end in it (A/B knob:
+// -1.8 % C4, -2.5 % C5)
+#ifndef RT_EARLY_DRAIN
+#define RT_EARLY_DRAIN 0
+#endif
 
 // the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
 #ifndef RT_COH_BVH_MIN_WAVES
@@ -346,7 +351,23 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         }
 #endif
         if (EXACT && __any(dleft != 0u)) {
-            if (dleft != 0u) drain_step(dleft);
+            if (dleft != 0u) {
+#if RT_EARLY_DRAIN
+                // a lane whose path ends in this iteration's service (the same decision) completes its
+                // previous fold here, before the iteration's stores: its ring loads then wait for no
+                // store of this iteration (vmcnt counts both)
+                bool ends = false;
+                if (in_path && (!BVH || (tiA >= NN && tiB >= NN))) {
+                    bool em = false;
+                    if (triA >= 0) em = S.mats[2 * f2i(S.tris[4 * triA].w)].w != 0.0f;
+                    ends = triA < 0 || em || (pend && !cont);
+                }
+                if (ends) drain_all(dleft);
+                else drain_step(dleft);
+#else
+                drain_step(dleft);
+#endif
+            }
         }
         // ======================= lane-level work queue (wave-collective) =======================
         // at the top of the iteration, before any store: a lane that finished its item in the previous
