@@ -22,6 +22,10 @@
 //
 // Rays with a non-finite reciprocal direction (an exactly axis-aligned component) have no monotone
 // slab test; such a ray walks the BVH on its own lane (the reference's traversal, rt_path.h).
+//
+// Scenes without decisive leaf boxes (C5: Cornell + a 79k-triangle mesh) use the BVH variant
+// (template argument BVH): same vertex loop, drain, parked samples and work pool, the scene in HBM,
+// and the lane's two rays walking the stackless BVH in the megakernel's postponed-leaf rounds.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -118,6 +118,23 @@ def test_row_band_split_reassembles_bitwise(ctx):
     assert np.array_equal(bits(full), bits(acc1))
 
 
+def test_row_band_split_reassembles_bitwise_bvh_variant():
+    """The same split on the C5 scene (the vertex kernel's BVH variant), frame chunks included."""
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell_c5(np.load(os.path.join(os.path.dirname(__file__), "golden", "bvh_scene.npz"))["raw_bunny"]))
+        W, H, spp = 64, 40, 12
+        rgba1, acc1 = render(c, W, H, spp, seed=9)
+        assert c.stats().kernel == 3
+        full = np.zeros_like(acc1)
+        for r in range(3):
+            rgba, acc = render(c, W, H, spp, seed=9, band=8, rank=r, nranks=3)
+            full[c.local_to_global_rows()] = acc
+        assert np.array_equal(bits(full), bits(acc1))
+    finally:
+        c.close()
+
+
 def test_matches_oracle_at_larger_size(ctx):
     W, H, spp = 192, 160, 32
     rgba, acc = render(ctx, W, H, spp, seed=5)
