@@ -176,6 +176,16 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_DRAIN_BATCH
 #define RT_DRAIN_BATCH 2
 #endif
+// fold ring layout: 1 = lane-major ([thread][position]: a lane's consecutive levels share cache
+// lines, so a drain read follows its push in L2), 0 = position-major ([position][thread]) (A/B knob)
+#ifndef RT_RING_LANE_MAJOR
+#define RT_RING_LANE_MAJOR 1
+#endif
+#if RT_RING_LANE_MAJOR
+#define RING_AT(p) ((size_t)gtid * Q.stack_depth + (p))
+#else
+#define RING_AT(p) ((size_t)(p) * Q.total_threads + gtid)
+#endif
 // complete the previous fold at the top of the iteration when the path will end in it (A/B knob:
 // -1.8 % C4, -2.5 % C5)
 #ifndef RT_EARLY_DRAIN
@@ -248,8 +258,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     auto drain_step = [&](uint32_t& dleft) {
         CKParams& Q = kargs4();
         const uint32_t pos = lsu(VS_DPOS);
-        const float4 e = Q.stack_ld[(size_t)pos * Q.total_threads + gtid];
-        const int m = Q.stack_mat[(size_t)pos * Q.total_threads + gtid];
+        const float4 e = Q.stack_ld[RING_AT(pos)];
+        const int m = Q.stack_mat[RING_AT(pos)];
         const float4 mb2 = S.mats[2 * m];
         const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
         const V3 L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(ls3(VS_DL), f), e.w), PDF), Q.rr));
@@ -278,8 +288,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
                 const uint32_t pj = pos >= j ? pos - j : pos + R - j;
                 const uint32_t at = j < dleft ? pj : pos;   // levels past the fold re-read the first one (unused)
-                e[j] = Q.stack_ld[(size_t)at * Q.total_threads + gtid];
-                m[j] = Q.stack_mat[(size_t)at * Q.total_threads + gtid];
+                e[j] = Q.stack_ld[RING_AT(at)];
+                m[j] = Q.stack_mat[RING_AT(at)];
             }
 #pragma unroll
             for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
@@ -479,8 +489,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         fits = (pos + R - lo) % R >= dleft;
                     }
                     if (fits) {
-                        Q.stack_ld[(size_t)pos * Q.total_threads + gtid] = e;
-                        Q.stack_mat[(size_t)pos * Q.total_threads + gtid] = pm;
+                        Q.stack_ld[RING_AT(pos)] = e;
+                        Q.stack_mat[RING_AT(pos)] = pm;
                     } else {
                         atomicAdd((unsigned long long*)&Q.counters[3], 1ull);   // reported as stack overflow
                     }
