@@ -68,6 +68,7 @@ struct rt_ctx {
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
+    bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
@@ -324,6 +325,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -567,6 +569,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 n_chunks = (nf + F - 1) / F;
                 Q.n_chunks = n_chunks; Q.chunk_frames = F; Q.items_per_chunk = (uint32_t)items_px;
                 Q.park_all = park_all ? 1u : 0u;
+                Q.lbuf_pixel_major = park_all && c->lbuf_pm ? 1u : 0u;
                 if (items_px * n_chunks >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
                 Q.n_items = (uint32_t)(items_px * n_chunks);
                 if (n_chunks > 1 || park_all) {

@@ -248,7 +248,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // samples and fold-level stores waited for their write-back.
     auto complete = [&](V3 L, uint32_t local, uint32_t fidx) {
         CKParams& Q = kargs4();
-        const size_t at = (((size_t)(fidx >> 2) * Q.lbuf_stride + local) * 4u + (fidx & 3u)) * 3u;
+        const size_t blk = Q.lbuf_pixel_major ? (size_t)local * ((Q.n_frames + 3u) >> 2) + (fidx >> 2)
+                                              : (size_t)(fidx >> 2) * Q.lbuf_stride + local;
+        const size_t at = (blk * 4u + (fidx & 3u)) * 3u;
         Q.lbuf[at] = L.x;
         Q.lbuf[at + 1] = L.y;
         Q.lbuf[at + 2] = L.z;

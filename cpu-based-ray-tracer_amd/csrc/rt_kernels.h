@@ -33,6 +33,8 @@ struct KParams {
     uint32_t n_chunks, chunk_frames, items_per_chunk;
     float* lbuf; size_t lbuf_stride;
     uint32_t park_all;              // every frame is parked (the vertex kernel): finalize accumulates all of them
+    uint32_t lbuf_pixel_major;      // park_all: a pixel's 4-frame blocks are contiguous ([pixel][block]) instead of
+                                    // [block][pixel] (lbuf_stride pixels apart)
     // outputs (compact local pixel order: local_row * W + x)
     float4* accum; uint32_t* rgba;
     // scratch

@@ -621,7 +621,8 @@ __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_
     float4 acc = (P.park_all && P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[i];
     const uint32_t nfp = P.park_all ? P.n_frames : P.n_frames - P.chunk_frames;
     for (uint32_t b = 0; b * 4u < nfp; ++b) {
-        const float4* blk = reinterpret_cast<const float4*>(P.lbuf + ((size_t)b * P.lbuf_stride + i) * 12u);
+        const size_t bi = (P.park_all && P.lbuf_pixel_major) ? (size_t)i * ((nfp + 3u) >> 2) + b : (size_t)b * P.lbuf_stride + i;
+        const float4* blk = reinterpret_cast<const float4*>(P.lbuf + bi * 12u);
         const float4 q0 = blk[0], q1 = blk[1], q2 = blk[2];
         const float v[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
         const uint32_t n = min(4u, nfp - b * 4u);
