@@ -60,7 +60,7 @@ struct rt_ctx {
     // frame chunking (KParams::n_chunks): split when a launch has fewer than min_px_per_lane pixels
     // per lane, into about items_per_lane items per lane but no chunk shorter than min_chunk_frames
     // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
-    uint32_t force_chunks = 0, items_per_lane = 48, min_px_per_lane = 32, min_chunk_frames = 32;
+    uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 16;
     uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch (RT_LBUF_BUDGET_MB); C4 needs 20 GB of 288
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
