@@ -17,6 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 
 RT_OK = 0
+RT_ERR_OVERFLOW = -6
 RENDER_EXACT = 1
 RENDER_COUNT = 2
 RENDER_GLOBAL_SCENE = 4
@@ -49,7 +50,7 @@ class Stats(C.Structure):
                 ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64), ("wave_fold", C.c_uint64),
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
                 ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
-                ("n_passes", C.c_uint32), ("kernel", C.c_uint32)]
+                ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64)]
 
 _DIAGNOSTIC = {"rt_debug_counters"}
 
@@ -123,6 +124,7 @@ def lib():
         "rt_debug_counters": (i32, [vp, C.POINTER(C.c_uint64), u32]),
         "rt_trace": (i32, [vp, u64, fp, fp, C.POINTER(i32), C.POINTER(C.c_double)]),
         "rt_math_selftest": (i32, [vp, u64, fp, fp]),
+        "rt_debug_primitives": (i32, [vp, u64, fp, C.POINTER(i32), C.POINTER(C.c_double), u64, fp, C.POINTER(i32)]),
         "rt_world_material_default": (None, [C.POINTER(WorldMaterial)]),
         "rt_scene_add_world_sphere": (i32, [vp, fp, C.c_float, C.POINTER(WorldMaterial), C.POINTER(i32)]),
         "rt_scene_add_world_mesh": (i32, [vp, fp, u32, C.POINTER(u32), u32, fp, C.POINTER(WorldMaterial), C.POINTER(i32)]),
@@ -474,6 +476,17 @@ class Context:
         self._check(lib().rt_world_trace(self.h, n, _fp(org), _fp(dirs), ent.ctypes.data_as(C.POINTER(C.c_int32)),
                                          tri.ctypes.data_as(C.POINTER(C.c_int32)), _fp(tb)), "rt_world_trace")
         return ent, tri, tb
+
+    def debug_primitives(self, mt_cases, box_cases):
+        """The kernels' Moller-Trumbore (float pre-screen + double test) and the three slab-test forms on the
+        reference's fixture layouts (rt_debug_primitives): (mt_hit, mt_t, box_hit[n, 3])."""
+        mt = np.ascontiguousarray(mt_cases, np.float32).reshape(-1, 15)
+        bx = np.ascontiguousarray(box_cases, np.float32).reshape(-1, 12)
+        mh = np.zeros(mt.shape[0], np.int32); mtt = np.zeros(mt.shape[0], np.float64); bh = np.zeros((bx.shape[0], 3), np.int32)
+        self._check(lib().rt_debug_primitives(self.h, mt.shape[0], _fp(mt), mh.ctypes.data_as(C.POINTER(C.c_int32)),
+                                              mtt.ctypes.data_as(C.POINTER(C.c_double)), bx.shape[0], _fp(bx),
+                                              bh.ctypes.data_as(C.POINTER(C.c_int32))), "rt_debug_primitives")
+        return mh, mtt, bh
 
     def math_selftest(self, x):
         x = np.ascontiguousarray(x, np.float32)

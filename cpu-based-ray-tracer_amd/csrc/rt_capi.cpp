@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +41,17 @@ struct rt_ctx {
     float4* d_stack_ld = nullptr;
     int32_t* d_stack_mat = nullptr;
     uint32_t stack_depth = 0;
+    uint32_t stack_depth_force = 0;   // test knob (RT_STACK_DEPTH): a small fold ring forces overflows
+    // EXACT: ring overflows listed by the vertex kernel and rendered again by resample_kernel
+    uint4* d_ovf = nullptr;
+    uint32_t ovf_cap = 1u << 20;
+    float4* d_rs_stack = nullptr;
+    int32_t* d_rs_mat = nullptr;
+    uint32_t rs_threads = 1024;
+    // counters[13] (lost levels / samples) and counters[14] (overflows listed and re-rendered) of the last render, copied
+    // to pinned host memory at the end of rt_render and checked at the next synchronisation
+    unsigned long long* h_ovf = nullptr;
+    bool pending_check = false;
     uint32_t grid = 0, block = 256, total_threads = 0;   // grid of the EXACT kernel (sizes the fold stack)
     uint32_t n_cu = 0;
     int occ_global[2][2] = {{0, 0}, {0, 0}};              // blocks per CU, [exact][count], scene in HBM
@@ -79,6 +91,19 @@ namespace {
 
 constexpr size_t kMaxLdsScene = 48 * 1024;   // scenes up to ~700 triangles live in LDS
 constexpr uint32_t kStackDepth = 192;   // EXACT fold stack; RR 0.8 => P(depth > 192) ~ 2.5e-19 per sample
+constexpr uint32_t kStackDepthMax = 2048;
+constexpr uint32_t kResampleDepth = 4096;   // the kernels' path-length cap (P = rr^4096)
+
+// levels of the EXACT fold stack / ring for survival probability rr: 1.5 x the depth a path exceeds with
+// probability 1e-12 (the vertex kernel's ring also holds the previous path's draining fold), at least
+// kStackDepth, at most kStackDepthMax.  Deeper paths are exact all the same: the vertex kernel lists
+// them for resample_kernel; the megakernel reports RT_ERR_OVERFLOW.
+uint32_t stack_levels_for(float rr)
+{
+    if (!(rr > 0.0f)) return kStackDepth;
+    const double d = 1.5 * std::ceil(std::log(1e-12) / std::log((double)rr));
+    return (uint32_t)std::min<double>(kStackDepthMax, std::max<double>(kStackDepth, d));
+}
 
 rt_status hip_fail(rt_ctx* c, hipError_t e, const char* what)
 {
@@ -99,6 +124,22 @@ template <class T> rt_status upload(rt_ctx* c, T*& dst, const std::vector<float>
     if (src.empty()) return RT_OK;
     HIPC(c, hipMalloc((void**)&dst, src.size() * sizeof(float)));
     HIPC(c, hipMemcpy((void*)dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+// after a stream synchronisation: an EXACT render that lost a fold level (megakernel stack) or a
+// sample the overflow list could not hold fails instead of returning a wrong image
+rt_status check_overflow(rt_ctx* c)
+{
+    if (!c->pending_check) return RT_OK;
+    c->pending_check = false;
+    c->stats.overflow_lost = c->h_ovf[0];
+    c->stats.resampled = c->h_ovf[1];
+    if (c->h_ovf[0] != 0) {
+        c->err = "EXACT fold stack overflow: " + std::to_string(c->h_ovf[0]) + " path level(s) or sample(s) lost (stack depth " +
+                 std::to_string(c->stack_depth) + ", rr too close to 1 for the megakernel's stack)";
+        return RT_ERR_OVERFLOW;
+    }
     return RT_OK;
 }
 
@@ -333,6 +374,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_MIN_CHUNK_FRAMES")) c->min_chunk_frames = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    if (const char* e = std::getenv("RT_STACK_DEPTH")) c->stack_depth_force = std::min<uint32_t>(kStackDepthMax, (uint32_t)std::strtoul(e, nullptr, 10));
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
     if (cfg && cfg->stream) {
@@ -344,7 +386,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess || hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev3) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 256) != hipSuccess) {
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 256) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_ovf, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
         return RT_ERR_HIP;
@@ -385,6 +428,8 @@ void rt_destroy(rt_ctx* c)
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev3) (void)hipEventDestroy(c->ev3);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
+    dfree(c->d_ovf); dfree(c->d_rs_stack); dfree(c->d_rs_mat);
+    if (c->h_ovf) (void)hipHostFree(c->h_ovf);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -448,10 +493,22 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     HIPC(c, hipSetDevice(c->device));
     const bool whitted = (p->flags & RT_RENDER_WHITTED) != 0;
     const bool exact = !whitted && (p->flags & RT_RENDER_EXACT) != 0, count = (p->flags & RT_RENDER_COUNT) != 0;
-    if (exact && !c->d_stack_ld) {
-        c->stack_depth = kStackDepth;
-        HIPC(c, hipMalloc((void**)&c->d_stack_ld, (size_t)c->stack_depth * c->total_threads * sizeof(float4)));
-        HIPC(c, hipMalloc((void**)&c->d_stack_mat, (size_t)c->stack_depth * c->total_threads * sizeof(int32_t)));
+    if (exact) {
+        // the fold stack / ring, sized from rr (reallocated when a render needs more levels)
+        const uint32_t want = c->stack_depth_force ? std::max<uint32_t>(1, c->stack_depth_force) : stack_levels_for(p->rr);
+        if (!c->d_stack_ld || want > c->stack_depth || (c->stack_depth_force && want != c->stack_depth)) {
+            HIPC(c, hipStreamSynchronize(c->stream));
+            dfree(c->d_stack_ld); dfree(c->d_stack_mat);
+            c->stack_depth = 0;
+            HIPC(c, hipMalloc((void**)&c->d_stack_ld, (size_t)want * c->total_threads * sizeof(float4)));
+            HIPC(c, hipMalloc((void**)&c->d_stack_mat, (size_t)want * c->total_threads * sizeof(int32_t)));
+            c->stack_depth = want;
+        }
+        if (!c->d_ovf) {
+            HIPC(c, hipMalloc((void**)&c->d_ovf, (size_t)c->ovf_cap * sizeof(uint4)));
+            HIPC(c, hipMalloc((void**)&c->d_rs_stack, (size_t)kResampleDepth * c->rs_threads * sizeof(float4)));
+            HIPC(c, hipMalloc((void**)&c->d_rs_mat, (size_t)kResampleDepth * c->rs_threads * sizeof(int32_t)));
+        }
     }
     KParams P{};
     P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes;
@@ -483,6 +540,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
     P.total_threads = c->total_threads;
     P.counters = c->d_counters;
+    P.ovf_list = exact ? c->d_ovf : nullptr; P.ovf_cap = c->ovf_cap;
+    P.rs_stack = c->d_rs_stack; P.rs_mat = c->d_rs_mat;
     P.thresh = c->thresh; P.steps = c->steps;
     P.force_walk = c->force_walk ? 1u : 0u;
     P.lds_pad = c->lds_pad;
@@ -585,8 +644,12 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local;
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
+                HIPC(c, hipMemsetAsync(c->d_counters + 3, 0, sizeof(unsigned long long), c->stream));   // this pass's overflow list
                 if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
+                // EXACT vertex kernel: the samples whose path outgrew the ring, rendered again into their
+                // parked slots (exits at once when none was listed)
+                if (coh && exact) HIPC(c, rt_launch_resample(Q, c->rs_threads, c->stream));
                 HIPC(c, rt_launch_finalize_chunks(Q, (uint32_t)px_local, c->stream));
                 c->stats.n_chunks = n_chunks;
                 done += nf;
@@ -597,6 +660,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh_bvh ? RT_KERNEL_VERTEX_BVH : coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);
         HIPC(c, hipEventRecord(c->ev1, c->stream));
         c->pending_stats = true;
+        if (exact && !whitted) {
+            // overflow outcome (listed total, lost), checked at the next synchronisation
+            HIPC(c, hipMemcpyAsync(c->h_ovf, c->d_counters + 13, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+            c->pending_check = true;
+        }
     }
     c->stats.samples = (uint64_t)c->local_rows * c->W * p->n_frames;
     if (out_rgba || out_accum) {
@@ -604,6 +672,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         if (out_rgba) HIPC(c, hipMemcpyAsync(out_rgba, c->d_rgba, npx * 4, hipMemcpyDeviceToHost, c->stream));
         if (out_accum) HIPC(c, hipMemcpyAsync(out_accum, c->d_accum, npx * 16, hipMemcpyDeviceToHost, c->stream));
         HIPC(c, hipStreamSynchronize(c->stream));
+        return check_overflow(c);
     }
     return RT_OK;
 }
@@ -730,7 +799,7 @@ rt_status rt_synchronize(rt_ctx* c)
 {
     if (!c) return RT_ERR_INVALID;
     HIPC(c, hipStreamSynchronize(c->stream));
-    return RT_OK;
+    return check_overflow(c);
 }
 
 rt_status rt_debug_counters(rt_ctx* c, uint64_t* out, uint32_t n)
@@ -749,14 +818,16 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_kernel_ms = ms;
-        unsigned long long h[16] = {};
+        unsigned long long h[16] = {};   // [3]: the last pass's overflow list; [13] lost, [14] listed in all passes
         HIPC(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
-        c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[3];
+        c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[13] + h[14];
         c->stats.wave_rounds = h[4]; c->stats.wave_steps = h[5]; c->stats.wave_tri_tests = h[6]; c->stats.wave_service = h[7];
         c->stats.wave_fold = h[8]; c->stats.cycles_service = h[9]; c->stats.cycles_queue = h[10]; c->stats.cycles_trace = h[11];
         c->stats.service_lanes = h[12];
         c->pending_stats = false;
     }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const rt_status ov = check_overflow(c);
     if (c->pending_denoise) {
         HIPC(c, hipEventSynchronize(c->ev3));
         float ms = 0.0f;
@@ -766,7 +837,7 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
     }
     c->stats.block = c->block; c->stats.stack_depth = c->stack_depth;
     *st = c->stats;
-    return RT_OK;
+    return ov;
 }
 
 rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t)
@@ -823,6 +894,32 @@ rt_status rt_world_trace(rt_ctx* c, uint64_t n, const float* org, const float* d
         (e = hipMemcpyAsync(tb, d_tb, n * 12, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         cleanup(); return hip_fail(c, e, "rt_world_trace");
+    }
+    cleanup();
+    return RT_OK;
+}
+
+rt_status rt_debug_primitives(rt_ctx* c, uint64_t n_mt, const float* mt, int32_t* mt_hit, double* mt_t, uint64_t n_box, const float* box,
+                              int32_t* box_hit)
+{
+    if (!c || (n_mt && (!mt || !mt_hit || !mt_t)) || (n_box && (!box || !box_hit))) return RT_ERR_INVALID;
+    if (n_mt > 0x7FFFFFFFull || n_box > 0x7FFFFFFFull) return RT_ERR_INVALID;
+    if (n_mt == 0 && n_box == 0) return RT_OK;
+    HIPC(c, hipSetDevice(c->device));
+    float *d_mt = nullptr, *d_box = nullptr; int32_t *d_mh = nullptr, *d_bh = nullptr; double* d_t = nullptr;
+    auto cleanup = [&]() { dfree(d_mt); dfree(d_box); dfree(d_mh); dfree(d_bh); dfree(d_t); };
+    hipError_t e = hipSuccess;
+    if ((n_mt && ((e = hipMalloc((void**)&d_mt, n_mt * 60)) != hipSuccess || (e = hipMalloc((void**)&d_mh, n_mt * 4)) != hipSuccess ||
+                  (e = hipMalloc((void**)&d_t, n_mt * 8)) != hipSuccess ||
+                  (e = hipMemcpyAsync(d_mt, mt, n_mt * 60, hipMemcpyHostToDevice, c->stream)) != hipSuccess)) ||
+        (n_box && ((e = hipMalloc((void**)&d_box, n_box * 48)) != hipSuccess || (e = hipMalloc((void**)&d_bh, n_box * 12)) != hipSuccess ||
+                   (e = hipMemcpyAsync(d_box, box, n_box * 48, hipMemcpyHostToDevice, c->stream)) != hipSuccess)) ||
+        (e = rt_launch_debug_primitives((uint32_t)n_mt, d_mt, d_mh, d_t, (uint32_t)n_box, d_box, d_bh, c->stream)) != hipSuccess ||
+        (n_mt && ((e = hipMemcpyAsync(mt_hit, d_mh, n_mt * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+                  (e = hipMemcpyAsync(mt_t, d_t, n_mt * 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess)) ||
+        (n_box && (e = hipMemcpyAsync(box_hit, d_bh, n_box * 12, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_debug_primitives");
     }
     cleanup();
     return RT_OK;

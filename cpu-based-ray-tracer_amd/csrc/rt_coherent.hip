@@ -442,6 +442,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             CKParams& Q = kargs4();
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
+            bool relisted = false;   // EXACT: the sample went to the overflow list (no fold, no parked store)
             V3 L{0.f, 0.f, 0.f};
             int mat = 0;
             bool emissive = false;
@@ -493,10 +494,18 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     if (fits) {
                         Q.stack_ld[RING_AT(pos)] = e;
                         Q.stack_mat[RING_AT(pos)] = pm;
+                        vertex = true;
                     } else {
-                        atomicAdd((unsigned long long*)&Q.counters[3], 1ull);   // reported as stack overflow
+                        // the path outgrew the ring: list the sample for the exact re-render
+                        // (rt_resample.hip) and end it here; its parked slot is written there
+                        const uint32_t slot = (uint32_t)atomicAdd((unsigned long long*)&Q.counters[3], 1ull);
+                        atomicAdd((unsigned long long*)&Q.counters[14], 1ull);
+                        const uint32_t frame = lsu(VS_FRAME);
+                        if (slot < Q.ovf_cap) Q.ovf_list[slot] = make_uint4(lsu(VS_LOCAL), frame - Q.first_frame, lsu(VS_PIX), frame);
+                        else atomicAdd((unsigned long long*)&Q.counters[13], 1ull);   // lost: rt_render reports it
+                        finished = true;
+                        relisted = true;
                     }
-                    vertex = true;
                 }
             } else if (triA < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
                 L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
@@ -576,7 +585,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 lsu(VS_FRAME) = frame + 1u;
                 const bool last = k == min(Q.chunk_frames, Q.n_frames - kbase);
                 if (last) have_pixel = false;
-                if (EXACT) {
+                if (EXACT && relisted) {
+                    // nothing to fold or park: resample_kernel writes this sample's slot
+                } else if (EXACT) {
 #if RT_SECTIONS
                     if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(7, 1);
 #endif
@@ -841,6 +852,49 @@ template __global__ void pt_coherent_kernel<true, false>(KParams);
 template __global__ void pt_coherent_kernel<false, false>(KParams);
 template __global__ void pt_coherent_kernel<true, true>(KParams);
 template __global__ void pt_coherent_kernel<false, true>(KParams);
+
+// ---------------------------------------------------------------------------------------------
+// device checks of the primitives the kernels shortcut (C-ABI rt_debug_primitives): the reference's
+// fixtures (zero-area triangles, zero / axis-aligned directions, parallel rays, NaN slabs) through
+//   * moller_trumbore_od with its float sign pre-test and |b2n| + |b3n| > |den| screen (rt_device.h)
+//     -- Whitted::RayTriangleIntersection, MC/TriangleMesh.h:19-45 -- on (a, b, c, o, d): E1 = b - a,
+//     E2 = c - a as the scene builder stores them;
+//   * AABB_3D::intersects_with_ray (MC/BoundingVolume.h:173-215) in the three forms the kernels use:
+//     slab_hit (std::max/min NaN rules), slab_hit_finite (IEEE max3/min3) and this file's box_hit
+//     (leaf boxes of the vertex kernel); the last two only for a finite reciprocal direction, where the
+//     kernels use them (-1 otherwise).
+__global__ void __launch_bounds__(256) debug_primitives_kernel(uint32_t n_mt, const float* __restrict__ mt, int32_t* __restrict__ mt_hit,
+                                                               double* __restrict__ mt_t, uint32_t n_box, const float* __restrict__ box,
+                                                               int32_t* __restrict__ box_out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_mt) {
+        const float* q = mt + 15 * (size_t)i;
+        const V3 a{q[0], q[1], q[2]}, b{q[3], q[4], q[5]}, c{q[6], q[7], q[8]}, o{q[9], q[10], q[11]}, d{q[12], q[13], q[14]};
+        double t = 0.0;
+        const bool h = moller_trumbore_od(a, sub(b, a), sub(c, a), o, d, t);
+        mt_hit[i] = h ? 1 : 0;
+        mt_t[i] = h ? t : 0.0;
+    }
+    if (i < n_box) {
+        const float* q = box + 12 * (size_t)i;
+        const Ray r = make_ray(V3{q[6], q[7], q[8]}, V3{q[9], q[10], q[11]});
+        box_out[3 * i] = slab_hit(r, q[0], q[1], q[2], q[3], q[4], q[5]) ? 1 : 0;
+        const bool fin = finite3(r.rcp);
+        const V3 s0{q[0] - r.o.x, q[1] - r.o.y, q[2] - r.o.z}, s1{q[3] - r.o.x, q[4] - r.o.y, q[5] - r.o.z};
+        box_out[3 * i + 1] = fin ? (slab_hit_finite(r, q[0], q[1], q[2], q[3], q[4], q[5]) ? 1 : 0) : -1;
+        box_out[3 * i + 2] = fin ? (box_hit(s0, s1, r.rcp) ? 1 : 0) : -1;
+    }
+}
+
+hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* mt_hit, double* mt_t, uint32_t n_box, const float* box,
+                                      int32_t* box_hit, hipStream_t stream)
+{
+    const uint32_t n = n_mt > n_box ? n_mt : n_box;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(debug_primitives_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n_mt, mt, mt_hit, mt_t, n_box, box, box_hit);
+    return hipGetLastError();
+}
 
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit)
 {

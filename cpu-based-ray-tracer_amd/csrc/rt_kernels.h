@@ -46,7 +46,13 @@ struct KParams {
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray
-    unsigned long long* counters;   // [node_tests, tri_tests, rays, stack_overflow]
+    unsigned long long* counters;   // [node_tests, tri_tests, rays, this pass's ring overflows (listed), ...,
+                                    //  [13] levels dropped (megakernel) or overflows the list could not hold,
+                                    //  [14] ring overflows listed in all passes]
+    // EXACT: samples whose path outgrew the vertex kernel's fold ring -- (local pixel, frame index,
+    // global pixel, frame) -- rendered again by resample_kernel with a deep stack (rt_resample.hip)
+    uint4* ovf_list; uint32_t ovf_cap;
+    float4* rs_stack; int32_t* rs_mat;
     // the Denoiser's G-buffer frame (set => pt_megakernel<..., GB = true>); one sample per pixel
     float4* gb_color; float4* gb_pos; float4* gb_nrm; int32_t* gb_prim; uint32_t gb_clamp;
 };
@@ -69,6 +75,13 @@ hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, u
 hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 hipError_t rt_launch_world_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* ent, int32_t* tri, float* tb,
                                  hipStream_t stream);
+// exact re-render of the listed ring overflows into their parked slots (before finalize)
+hipError_t rt_launch_resample(const KParams& P, uint32_t threads, hipStream_t stream);
+// device checks of the two primitives with shortcuts (rt_coherent.hip): Moller-Trumbore with its float
+// pre-screen on (a, b, c, o, d) cases (hit, t); the slab test on (lo, hi, o, d) cases in its three forms
+// (general, finite-reciprocal, the vertex kernel's leaf-box form; -1 where a form does not apply)
+hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* mt_hit, double* mt_t, uint32_t n_box, const float* box,
+                                      int32_t* box_hit, hipStream_t stream);
 hipError_t rt_launch_finalize_chunks(const KParams& P, uint32_t n_px, hipStream_t stream);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);

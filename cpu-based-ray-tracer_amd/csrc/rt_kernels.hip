@@ -191,7 +191,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                         Q.stack_ld[(size_t)lvl * Q.total_threads + gtid] = e;
                         Q.stack_mat[(size_t)lvl * Q.total_threads + gtid] = pend_mat;
                     } else {
-                        atomicAdd((unsigned long long*)&Q.counters[3], 1ull);   // reported as stack overflow
+                        // a level the stack cannot hold (sized from rr, rt_capi.cpp): counted, and rt_render
+                        // reports the render as failed (RT_ERR_OVERFLOW) instead of returning a wrong sample
+                        atomicAdd((unsigned long long*)&Q.counters[13], 1ull);
                     }
                 }
                 if (!finished) {

@@ -43,6 +43,7 @@ typedef int32_t rt_status;
 #define RT_ERR_IO (-3)      /* file not found / unparsable OBJ */
 #define RT_ERR_STATE (-4)   /* call order (no scene uploaded, no viewport) */
 #define RT_ERR_OOM (-5)     /* device allocation failed */
+#define RT_ERR_OVERFLOW (-6) /* an EXACT render lost a path level (see rt_render): the image is not the reference's */
 
 typedef struct rt_scene rt_scene; /* host-side scene builder */
 typedef struct rt_ctx rt_ctx;     /* one device context (one GPU, one stream) */
@@ -159,7 +160,16 @@ typedef struct {
  * packs RGBA8.  Asynchronous on the context stream unless a host output pointer is given:
  * out_rgba (local rows x width u32, ABGR, may be NULL) / out_accum (local rows x width x 4 f32,
  * may be NULL) are filled after a stream synchronisation.  Local row r is global row
- * (rank + (r / band) * nranks) * band + r % band. */
+ * (rank + (r / band) * nranks) * band + r % band.
+ *
+ * Path length (RT_RENDER_EXACT): Renderer::shading recurses until Russian roulette stops it
+ * (MC/Renderer.cpp:193); the kernels cut a path at 4096 vertices (probability rr^4096: 1e-397 at the
+ * default 0.8, 1.3e-18 at 0.99).  The fold stack is sized from rr (1.5 x the depth a path exceeds with
+ * probability 1e-12, 192..2048 levels); a deeper path is still exact -- the vertex kernel lists the
+ * sample and renders it again with a 4096-level stack (rt_stats.resampled).  Only when a level cannot be
+ * kept (the megakernel's stack, used for G-buffer/counter renders, or more than 2^20 overflows in one
+ * pass) does the render fail: RT_ERR_OVERFLOW, returned by the call that synchronises with it (rt_render
+ * with an output pointer, rt_synchronize, rt_get_stats). */
 rt_status rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint32_t* out_rgba, float* out_accum);
 /* device pointers of the local accumulation (float4) and RGBA8 buffers */
 rt_status rt_device_buffers(rt_ctx* ctx, void** d_accum, void** d_rgba);
@@ -173,7 +183,7 @@ typedef struct {
     uint64_t node_tests;      /* RT_RENDER_COUNT only */
     uint64_t tri_tests;
     uint64_t rays;
-    uint64_t stack_overflows; /* paths deeper than the EXACT fold stack (expected 0) */
+    uint64_t stack_overflows; /* EXACT paths deeper than the fold stack / ring: resampled + overflow_lost */
     uint64_t samples;
     uint32_t grid, block, stack_depth;
     /* RT_RENDER_COUNT scheduling diagnostics: wave-level executions */
@@ -186,6 +196,8 @@ typedef struct {
                                  launch has few pixels per lane; last_kernel_ms covers the in-order finalize */
     uint32_t n_passes;        /* launches over consecutive frame ranges (bounded parked-sample memory) */
     uint32_t kernel;          /* the path kernel of the last rt_render: RT_KERNEL_* */
+    uint64_t resampled;       /* EXACT: samples whose path outgrew the fold ring, rendered again exactly */
+    uint64_t overflow_lost;   /* EXACT: levels / samples that could not be kept (non-zero => RT_ERR_OVERFLOW) */
 } rt_stats;
 #define RT_KERNEL_MEGA 0      /* pt_megakernel (rt_kernels.hip): any scene, counters, G-buffer frames */
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */
@@ -226,6 +238,15 @@ rt_status rt_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, 
 /* closest hit of n rays against a Whitted world (get_intersection_payload, WH/Renderer.h:109-140):
  * entity index or -1, mesh triangle slot or -1, and (t, barycentric 2, barycentric 3) as 3 floats */
 rt_status rt_world_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* entity, int32_t* tri, float* t_bary);
+/* device checks of the primitives the kernels shortcut, on the reference's fixture layouts:
+ * n_mt Moller-Trumbore cases of 15 floats (a, b, c, origin, direction; MC/TriangleMesh.h:19-45) ->
+ * mt_hit (0/1) and mt_t (the double t on a hit, else 0) through the kernels' float pre-screen +
+ * double test; n_box slab cases of 12 floats (min, max, origin, direction; MC/BoundingVolume.h:173-215)
+ * -> box_hit, 3 per case: the std::max/min form, the finite-reciprocal IEEE form and the vertex
+ * kernel's leaf-box form (-1 for the last two when the reciprocal direction is not finite).
+ * Host arrays; any count may be 0. */
+rt_status rt_debug_primitives(rt_ctx* ctx, uint64_t n_mt, const float* mt_cases, int32_t* mt_hit, double* mt_t, uint64_t n_box,
+                              const float* box_cases, int32_t* box_hit);
 /* device arithmetic self-test: for each x: sqrtf, 1/x, cos, sin (as the kernel evaluates them),
  * the double reciprocal's low/high words, and the C1 specular lobe powf(x, 25) -> 7 floats per input */
 rt_status rt_math_selftest(rt_ctx* ctx, uint64_t n, const float* x, float* out);

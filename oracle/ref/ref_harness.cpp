@@ -40,6 +40,7 @@
 #include <thread>
 #include <atomic>
 #include <optional>
+#include <chrono>
 #include <glm/glm.hpp>
 #include <glm/gtc/matrix_transform.hpp>
 #define private public
@@ -502,6 +503,64 @@ static int cmd_image_mt(const char* dir, uint32_t W, uint32_t H, uint32_t spp, f
     return 0;
 }
 
+// CPU BASELINE timing (bench.py cpu_baseline, tools/cpu_reference_configs.py): the reference's work per
+// frame with its SHIPPED random stream -- thread_local std::mt19937 default-seeded 5489 behind the MSVC
+// 32-bit distribution (WN/Random.h:27-30,47-48, WN/Random.cpp:5-6), no injection -- on a persistent
+// pool of `threads` std::threads (the std::execution::par row loop of Renderer::Render,
+// MC/Renderer.cpp:100-110; a pool created once, so no thread re-seeds its engine per frame, SURVEY.md
+// section 8(c) pitfall).  Per frame and pixel: the jittered camera direction (Camera::
+// RecomputeRayDirections' loop body, MC/Camera.cpp:119-125 -- run row-parallel here; the reference runs
+// it serially on the UI thread, which would only make the baseline slower), RayGen_Shader (cast_path,
+// accum += color, accum / frame, clamp, ABGR pack: MC/Renderer.cpp:124-134).  Frames are separated by a
+// barrier, as consecutive Render() calls are.  Prints one line: samples, seconds (scene build excluded).
+static int cmd_bench_mt(const char* dir, const char* extra, uint32_t W, uint32_t H, uint32_t spp, float rr, int threads)
+{
+    Scene* s = build_cornell(dir, split_extra(extra));
+    Camera cam{35.0f, 0.1f, 100.0f};
+    cam.ResizeViewport(W, H);
+    Hybrid h{s, rr};
+    std::vector<glm::vec4> acc((size_t)W * H, glm::vec4(0.0f));
+    std::vector<uint32_t> rgba((size_t)W * H, 0);
+    std::vector<std::atomic<uint32_t>> next(spp + 1);
+    for (auto& a : next) a.store(0);
+    std::atomic<int> arrived{0};
+    std::atomic<uint32_t> generation{0};
+    auto barrier = [&]() {   // sense-reversing spin barrier between frames (Render() calls)
+        const uint32_t g = generation.load();
+        if (arrived.fetch_add(1) + 1 == threads) { arrived.store(0); generation.fetch_add(1); }
+        else while (generation.load() == g) std::this_thread::yield();
+    };
+    auto worker = [&]() {
+        set_msvc_distribution();   // the shipped engine of this thread: default-seeded (5489), never re-seeded
+        std::vector<glm::vec3> row(W);
+        for (uint32_t f = 1; f <= spp; ++f) {
+            for (;;) {
+                const uint32_t y = next[f].fetch_add(1);
+                if (y >= H) break;
+                for (uint32_t x = 0; x < W; ++x) row[x] = camera_dir(cam, x, y, W, H);
+                for (uint32_t x = 0; x < W; ++x) {
+                    const size_t px = (size_t)y * W + x;
+                    acc[px] += glm::vec4{h.cast_path(AccelerationStructure::Ray{cam.Position(), Whitted::normalize(row[x])}), 1.0f};
+                    glm::vec4 fin = acc[px] / (float)f;
+                    fin = glm::clamp(fin, glm::vec4(0.0f), glm::vec4(1.0f));
+                    rgba[px] = vecRGBA_to_0xABGR(fin);
+                }
+            }
+            barrier();
+        }
+    };
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> ts;
+    for (int i = 0; i < threads; ++i) ts.emplace_back(worker);
+    for (auto& t : ts) t.join();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    uint64_t chk = 0;
+    for (uint32_t v : rgba) chk += v;
+    printf("bench_mt samples %llu seconds %.6f threads %d checksum %llu\n", (unsigned long long)((uint64_t)W * H * spp), sec, threads,
+           (unsigned long long)chk);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
     check_layout_once();
@@ -518,6 +577,8 @@ int main(int argc, char** argv)
     if (c == "camera" && argc == 7) return cmd_camera(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), strtoull(argv[5], 0, 10), argv[6]);
     if (c == "image_mt" && argc == 8)
         return cmd_image_mt(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), (float)atof(argv[6]), argv[7]);
+    if (c == "bench_mt" && argc == 9)
+        return cmd_bench_mt(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), (float)atof(argv[7]), atoi(argv[8]));
     if (c == "image" && argc == 13)
         return cmd_image(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), strtoull(argv[7], 0, 10), (float)atof(argv[8]), atoi(argv[9]),
                          argv[10], argv[11], argv[12]);
