@@ -26,12 +26,44 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 
-# Algorithmic bytes per sample for the C4 Cornell workload (DESIGN.md
-# "Measurement"): reference work per sample = 3.645 rays x (24.61 node tests x 32 B + 3.57 triangle
-# tests x 36 B + 16 B shading fetch).
-REF_WORK = {"rays_per_sample": 3.645, "node_tests_per_ray": 24.61, "tri_tests_per_ray": 3.57}
+# The reference's work per C4 sample (oracle work counters at 1920x1080, seed 0,
+# RR 0.8, which agree with SURVEY's instrumented reference): rays, BVH node (AABB) tests per ray,
+# Moller-Trumbore tests per ray, shading calls.  Priced per SURVEY 8(d): node = 32 B / 18 flop, triangle
+# = 36 B / 54 flop (fp32-equivalent, incl. the fp64 part), shading = 16 B fetch / 150 flop.
+REF_WORK = {"rays_per_sample": 3.6475, "node_tests_per_ray": 24.619, "tri_tests_per_ray": 3.574, "shading_calls_per_sample": 1.4723}
 BYTES_PER_SAMPLE = REF_WORK["rays_per_sample"] * (REF_WORK["node_tests_per_ray"] * 32 + REF_WORK["tri_tests_per_ray"] * 36 + 16)
-HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FLOPS_PER_SAMPLE = (REF_WORK["rays_per_sample"] * (REF_WORK["node_tests_per_ray"] * 18 + REF_WORK["tri_tests_per_ray"] * 54)
+                    + REF_WORK["shading_calls_per_sample"] * 150)
+# MI355X_MICROARCH.md / SURVEY.md 8(d): FP32 vector peak (dense, packed-FMA issue) and HBM3E peak
+VALU_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+# VALU issue peak: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md),
+# 256 CUs x 4 SIMDs at 2.4 GHz
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
+
+
+def lib_digest(path):
+    import hashlib
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def counter_pass(kind, W, H, spp, exact, world, passes, digest):
+    """The PMC summary of a rocprofv3 counter pass of THIS build (sha-256 of librt_hip.so) on THIS shape,
+    if one is committed under profiles/ (profiles/run_rocprof.sh + profiles/summarize_pmc.py); else None."""
+    import glob
+    key = f"{kind}:{W}x{H}x{spp}_{'exact' if exact else 'fast'}_n{world}_p{passes}"
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "**", "pmc_summary*.json"), recursive=True), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("key") == key and digest is not None and d.get("lib_sha256") == digest:
+            d["_file"] = os.path.relpath(p, REPO)
+            return d
+    return None
 
 
 def load_pkg():
@@ -50,49 +82,89 @@ def load_dist():
     return m
 
 
-def cpu_baseline(W, H, seconds, threads):
-    """The reference renderer (oracle/_ref: the reference's BVH/triangle/material/camera code compiled
-    from /root/reference, integrator glue restated) on this host's cores, bounded to ~`seconds`;
-    falls back to the oracle restatement ("port") if the harness binary is absent."""
+def host_cpu():
+    """The host CPU this job runs on: model, sockets, physical cores per socket (sysfs), and the CPUs
+    this job may use (affinity, cgroup quota, OMP_NUM_THREADS -- 16 on a one-GPU box)."""
+    def read(p):
+        try:
+            return open(p).read().strip()
+        except OSError:
+            return None
+    model = None
+    for line in (read("/proc/cpuinfo") or "").splitlines():
+        if line.startswith("model name"):
+            model = line.split(":", 1)[1].strip()
+            break
+    pk = {}
+    for c in range(os.cpu_count() or 0):
+        pkg = read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id")
+        core = read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id")
+        if pkg is not None:
+            pk.setdefault(pkg, set()).add(core)
+    usable = len(os.sched_getaffinity(0))
+    quota = read("/sys/fs/cgroup/cpu.max")
+    if quota and quota.split()[0] != "max":
+        q, per = quota.split()
+        usable = min(usable, max(1, int(int(q) / int(per))))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        usable = min(usable, omp)
+    per_socket = max((len(v) for v in pk.values()), default=usable)
+    return {"model": model, "sockets": len(pk) or 1, "physical_cores_per_socket": per_socket, "usable_cpus": usable}
+
+
+def cpu_baseline(W, H, seconds):
+    """The reference renderer timed on this host's cores (SURVEY.md section 8(d) "CPU baseline").
+
+    oracle/_ref/ref_harness bench_mt: the reference's MC/ camera, BVH, triangle and material code compiled
+    from /root/reference (integrator glue restated, MC/Renderer.cpp:91-214) with its SHIPPED random
+    stream -- thread_local std::mt19937 default-seeded, MSVC 32-bit distribution (WN/Random.h:27-30,47-48,
+    WN/Random.cpp:5-6), no injection -- on a persistent pool of one thread per CPU this job may use (the
+    std::execution::par row loop of Renderer::Render, MC/Renderer.cpp:100-110).  The measured rate is
+    `value` (cores = the threads used); `socket_estimate` scales the measured per-thread rate to one
+    thread per physical core of one socket, the baseline BASELINE.json's target is quoted against
+    (linear: the Cornell scene is cache-resident and pixels are independent; the per-thread rate at the
+    job's full CPU share already carries the all-core clock)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    if os.path.exists(harness):
-        tmp = tempfile.mkdtemp(prefix="rt_cpu_")
-        try:
-            for (name, raw, _, _) in O.cornell_meshes():   # the fixture's objl positions, written back as OBJ
-                with open(os.path.join(tmp, name + ".obj"), "w") as f:
-                    for v in raw.reshape(-1, 3):
-                        f.write("v %r %r %r\n" % tuple(float(c) for c in v))
-                    for i in range(raw.shape[0]):
-                        f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
+    if not os.path.exists(harness):
+        return None
+    cpu = host_cpu()
+    threads = cpu["usable_cpus"]
+    tmp = tempfile.mkdtemp(prefix="rt_cpu_")
+    try:
+        for (name, raw, _, _) in O.cornell_meshes():   # the fixture's objl positions, written back as OBJ
+            with open(os.path.join(tmp, name + ".obj"), "w") as f:
+                for v in raw.reshape(-1, 3):
+                    f.write("v %r %r %r\n" % tuple(float(c) for c in v))
+                for i in range(raw.shape[0]):
+                    f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
 
-            def run(spp):
-                out = [os.path.join(tmp, x) for x in ("a", "r", "s")]
-                t0 = time.perf_counter()
-                subprocess.run([harness, "image", tmp, "", str(W), str(H), str(spp), "0", "0.8", str(threads)] + out,
-                               check=True, capture_output=True)
-                return time.perf_counter() - t0
+        def run(spp):
+            r = subprocess.run([harness, "bench_mt", tmp, "", str(W), str(H), str(spp), "0.8", str(threads)],
+                               check=True, capture_output=True, text=True)
+            tok = r.stdout.split()
+            return int(tok[2]), float(tok[4])   # samples, seconds (the frames only; scene build excluded)
 
-            t1 = run(1)
-            spp = max(1, int(seconds / max(t1, 1e-3)))
-            dt = run(spp)
-            return {"value": W * H * spp / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "reference",
-                    "sample": f"oracle/_ref/ref_harness: reference MC/ BVH+triangle+material+camera code (compiled from "
-                              f"/root/reference), integrator glue restated; Cornell {W}x{H} x {spp} spp = "
-                              f"{W * H * spp} samples in {dt:.1f} s, {threads} threads, RR 0.8"}
-        finally:
-            shutil.rmtree(tmp, ignore_errors=True)
-    sc = O.Scene()
-    t0 = time.perf_counter()
-    sc.render(W, H, 1, threads=threads)
-    t1 = time.perf_counter() - t0
-    spp = max(1, int(seconds / max(t1, 1e-3)))
-    t0 = time.perf_counter()
-    sc.render(W, H, spp, threads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": W * H * spp / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle restatement, Cornell {W}x{H} x {spp} spp in {dt:.1f} s, {threads} threads"}
+        n1, t1 = run(max(1, threads // 4))
+        spp = max(1, int(seconds * n1 / max(t1, 1e-3) / (W * H)))
+        n, dt = run(spp)
+        rate = n / dt / 1e6
+        per_thread = rate / threads
+        est = per_thread * cpu["physical_cores_per_socket"]
+        return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
+                "rng": "shipped (thread_local mt19937 seed 5489, MSVC 32-bit distribution, persistent pool)",
+                "cpu_model": cpu["model"], "sockets": cpu["sockets"],
+                "physical_cores_per_socket": cpu["physical_cores_per_socket"],
+                "socket_estimate": {"value": round(est, 2), "threads": cpu["physical_cores_per_socket"],
+                                    "how": f"measured {per_thread:.4f} Msamples/s per thread at {threads} threads x "
+                                           f"{cpu['physical_cores_per_socket']} physical cores of one socket (linear)"},
+                "sample": f"oracle/_ref/ref_harness bench_mt: the reference's MC/ BVH, triangle, material and camera code "
+                          f"(compiled from /root/reference), integrator glue restated, shipped RNG; Cornell {W}x{H} x "
+                          f"{spp} spp = {n} samples in {dt:.1f} s on {threads} threads (this job's CPU share), RR 0.8"}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():
@@ -105,7 +177,7 @@ def main():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--band", type=int, default=8)
     ap.add_argument("--fast", action="store_true", help="forward accumulation instead of the exact inner-first fold")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -172,35 +244,46 @@ def main():
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
 
-    # roofline of the megakernel on this rank: algorithmic bytes per launch / mean launch time.  A step
-    # is `passes` launches over consecutive frame ranges (each followed by the in-order finalize of its
-    # frame chunks, included in the HIP-event time); per launch = per step / passes.
+    # roofline of the path-tracing kernel on this rank.  SURVEY.md 8(d): there is no dense contraction
+    # and the Cornell scene lives on chip, so the binding roof for C2/C4 is the vector ALU; the sample is
+    # priced by the REFERENCE's work (FLOPS_PER_SAMPLE), whatever the kernel prunes.  achieved = flops per
+    # launch / the kernel's mean launch time (HIP events on the kernel's stream, rt_stats.last_kernel_ms;
+    # a step is `passes` launches over consecutive frame ranges, each with its in-order finalize).
     local_samples = gat.n_local * W * spp
     passes = max(1, int(launch_info.get("passes", 1)))
     k_s = float(np.mean(kernel_ms)) / 1e3 / passes if kernel_ms else float("nan")
     per_launch = local_samples / passes
-    achieved = BYTES_PER_SAMPLE * per_launch / k_s / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": launch_info.get("kernel", "?"), "kernel_ms": round(k_s * 1e3, 3),
-            "bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "samples_per_launch": int(per_launch),
-            "launches_per_step": passes, "frame_chunks": int(launch_info.get("chunks", 1)),
-            "gsamples_per_s_kernel": round(per_launch / k_s / 1e9, 4)}
-    prof = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(prof):
-        try:
-            pm = json.load(open(prof))
-            key = f"{roof['kernel']}:{W}x{H}x{spp}_{'fast' if args.fast else 'exact'}_n{world}_p{passes}"
-            if key in pm:
-                roof["traffic"] = pm[key]["hbm_bytes_per_launch"]
-        except Exception:
-            pass
+    tflops = FLOPS_PER_SAMPLE * per_launch / k_s / 1e12
+    alg_gbs = BYTES_PER_SAMPLE * per_launch / k_s / 1e9
+    kname = launch_info.get("kernel", "?")
+    digest = lib_digest(os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so"))
+    pmc = counter_pass(kname, W, H, spp, not args.fast, world, passes, digest)
+    roof = {"bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": kname, "kernel_ms": round(k_s * 1e3, 3), "flops_per_sample": round(FLOPS_PER_SAMPLE, 1),
+            "samples_per_launch": int(per_launch), "launches_per_step": passes,
+            "frame_chunks": int(launch_info.get("chunks", 1)), "gsamples_per_s_kernel": round(per_launch / k_s / 1e9, 4),
+            "reference_work": REF_WORK,
+            # secondary, labelled: the reference's algorithmic bytes against HBM.  > 1 is possible and means
+            # HBM is not the binding roof -- those bytes are LDS / scalar-cache reads of an on-chip scene
+            "hbm_algorithmic": {"bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "achieved_gbs": round(alg_gbs, 1),
+                                "peak_gbs": HBM_PEAK_GBS, "frac": round(alg_gbs / HBM_PEAK_GBS, 4)},
+            "lib_sha256": digest, "counters": None}
+    if pmc is not None:
+        # a rocprofv3 counter pass of this build and shape (profiles/): HBM bytes per launch and the
+        # kernel's VALU issue fraction / lane utilization
+        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        roof["counters"] = {"file": pmc["_file"], "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
+                            "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
+                            "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample"),
+                            "kernel_ms_profiled": pmc.get("kernel_ms")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        threads = min(threads, 16)
-        cpu = cpu_baseline(W, H, args.cpu_seconds, threads)
+        cpu = cpu_baseline(W, H, args.cpu_seconds)
+        if cpu is not None:
+            cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
+            cpu["gpu_over_socket_estimate"] = round(value / cpu["socket_estimate"]["value"], 1)
 
     if rank == 0:
         line = {
