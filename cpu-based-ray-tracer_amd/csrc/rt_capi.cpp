@@ -386,7 +386,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess || hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev3) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 256) != hipSuccess ||
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 512) != hipSuccess ||
         hipHostMalloc((void**)&c->h_ovf, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
@@ -586,7 +586,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const uint64_t px_local = (uint64_t)c->local_rows * c->W;
     const uint64_t items_px = P.n_items;   // 8x8-tile-padded pixel items
     c->last_flags = p->flags;
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 256, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 512, c->stream));
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
         if (whitted && c->hdr.n_went > 0) {
@@ -804,7 +804,7 @@ rt_status rt_synchronize(rt_ctx* c)
 
 rt_status rt_debug_counters(rt_ctx* c, uint64_t* out, uint32_t n)
 {
-    if (!c || !out || n > 32) return RT_ERR_INVALID;
+    if (!c || !out || n > 64) return RT_ERR_INVALID;
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(out, c->d_counters, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;

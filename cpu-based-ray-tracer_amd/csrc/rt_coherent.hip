@@ -159,6 +159,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_SECTIONS
 #define RT_SECTIONS 0
 #endif
+// event counts of a sections build: [0] wave iterations, [1] lanes on a path, [2] vertex lanes,
+// [3] finishing lanes, [4] camera lanes, [5] MT loop wave iterations, [6] MT lanes tested,
+// [7] (lane, candidate) pairs, [8] 64-pair chunks if compacted, [9] finishing wave iterations with a
+// fold still draining, [10] lanes finishing with a fold still draining, [11] lanes draining at the top,
+// [12] MT lanes on ray A, [13] ray A pairs, [14] MT hits (fp64 part passed), [15] scratch
+#define RT_SEC_COUNTS 16
 #ifndef RT_PAD_VALU
 #define RT_PAD_VALU 0
 #endif
@@ -171,6 +177,33 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // as written 14 VGPRs spill at 8 waves per SIMD: -6 %)
 #ifndef RT_MT_PREFETCH
 #define RT_MT_PREFETCH 0
+#endif
+// Moller-Trumbore loop: two candidates per iteration in packed f32 halves (A/B knob: 1 = A and B
+// candidates mixed, 2 = ray A's then ray B's with a splat direction).  At 8 waves per SIMD the packed
+// temporaries spill (2: 25 VGPRs): 5926 -> 5354 Msamples/s
+#ifndef RT_MT_X2
+#define RT_MT_X2 0
+#endif
+#ifndef RT_MT_X2_STAGED
+#define RT_MT_X2_STAGED 1
+#endif
+#if RT_MT_X2_STAGED
+#define RT_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define RT_SCHED_BARRIER() do { } while (0)
+#endif
+// a path that ends while the previous fold still drains: its fold starts at the top of the next
+// iteration (1) instead of completing the previous fold at once after the iteration's stores (0);
+// A/B: 5926 -> 5650 Msamples/s (slower, as the early drain)
+#ifndef RT_DEFER_FOLD
+#define RT_DEFER_FOLD 0
+#endif
+// fold levels drained per iteration at the top of the loop, their ring loads issued together: a fold
+// then rarely still drains when the next path ends (where completing it waits on loads issued after
+// the iteration's stores).  C4 1024 spp: 1 level 5935, 2 6117, 3 6198, 4 6195 Msamples/s
+// (tools/ab_libs.py, profiles/r02/ab/ab_drain_depth.json)
+#ifndef RT_DRAIN_STEP
+#define RT_DRAIN_STEP 3
 #endif
 // ring levels loaded together when a fold is completed at once (drain_all; A/B knob)
 #ifndef RT_DRAIN_BATCH
@@ -259,6 +292,39 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // (MC/Renderer.cpp:208,213), inner level first
     auto drain_step = [&](uint32_t& dleft) {
         CKParams& Q = kargs4();
+#if RT_DRAIN_STEP > 1
+        {   // up to RT_DRAIN_STEP levels per iteration, their ring loads issued together
+            const uint32_t R = Q.stack_depth;
+            uint32_t pos = lsu(VS_DPOS);
+            float4 e[RT_DRAIN_STEP];
+            int m[RT_DRAIN_STEP];
+#pragma unroll
+            for (uint32_t j = 0; j < RT_DRAIN_STEP; ++j) {
+                const uint32_t pj = pos >= j ? pos - j : pos + R - j;
+                const uint32_t at = j < dleft ? pj : pos;
+                e[j] = Q.stack_ld[RING_AT(at)];
+                m[j] = Q.stack_mat[RING_AT(at)];
+            }
+            V3 L = ls3(VS_DL);
+#pragma unroll
+            for (uint32_t j = 0; j < RT_DRAIN_STEP; ++j) {
+                if (j < dleft) {
+                    const float4 mb2 = S.mats[2 * m[j]];
+                    const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
+                    L = add(V3{e[j].x, e[j].y, e[j].z}, divs(divs(muls(mul(L, f), e[j].w), PDF), Q.rr));
+                }
+            }
+            const uint32_t n = dleft < RT_DRAIN_STEP ? dleft : RT_DRAIN_STEP;
+            dleft -= n;
+            if (dleft == 0u) {
+                complete(L, lsu(VS_DT0), lsu(VS_DT1));
+            } else {
+                st3(VS_DL, L);
+                lsu(VS_DPOS) = pos >= n ? pos - n : pos + R - n;
+            }
+            return;
+        }
+#endif
         const uint32_t pos = lsu(VS_DPOS);
         const float4 e = Q.stack_ld[RING_AT(pos)];
         const int m = Q.stack_mat[RING_AT(pos)];
@@ -335,6 +401,23 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
     uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     if (EXACT) lsu(VS_BASE) = 0u;
+#if RT_DEFER_FOLD
+    // a finished path's fold recorded for the top of the next iteration (the previous fold still drained)
+    bool deferred = false;
+    auto start_deferred = [&]() {
+        CKParams& Q = kargs4();
+        drain_all(dleft);   // the previous fold completes first
+        const uint32_t R = Q.stack_depth;
+        const uint32_t m = lsu(VS_PCOS);
+        const uint32_t nb = lsu(VS_BASE);
+        st3(VS_DL, ls3(VS_LD));
+        lsu(VS_DPOS) = (nb == 0u ? R : nb) - 1u;   // the innermost level, just below the next path's base
+        lsu(VS_DT0) = lsu(VS_LOCAL);
+        lsu(VS_DT1) = lsu(VS_FRAME) - 1u - Q.first_frame;
+        dleft = m;
+        deferred = false;
+    };
+#endif
     // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
     const uint32_t NN = S.n_nodes;
     uint32_t tiA = NN, tiB = NN;
@@ -344,13 +427,18 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint64_t sec_t = clock64();
     int sec_cur = 7;
 #define SEC_MARK(k) do { const uint64_t t_ = clock64(); sec_cyc[sec_cur] += t_ - sec_t; sec_t = t_; sec_cur = (k); } while (0)
-    // lane activity: [0] wave iterations, [1] lanes on a path, [2] vertex lanes, [3] finishing lanes,
-    // [4] camera lanes, [5] MT loop wave iterations, [6] MT tests (lanes), [7] fold wave iterations
-    uint64_t sec_n[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // wave-level event counts in the wave's LDS slot (RT_SEC_COUNTS words, written by the wave's first
+    // active lane; tools/prof_one.py --sections names them)
+    __shared__ uint32_t sec_cnt[4][RT_SEC_COUNTS];
+    uint32_t* const sec_w = sec_cnt[threadIdx.x >> 6];
+    if (lane < RT_SEC_COUNTS) sec_w[lane] = 0u;
     bool dbg_vertex = false, dbg_fin = false, dbg_cam = false;
-#define SEC_COUNT(i, v) do { sec_n[i] += (v); } while (0)
+    auto sec_first = [&]() { return lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1); };
+#define SEC_COUNT(i, v) do { const uint32_t v_ = (v); if (sec_first()) sec_w[i] += v_; } while (0)
+#define SEC_SUM(i, v) do { atomicAdd(&sec_w[i], (uint32_t)(v)); } while (0)
 #else
 #define SEC_COUNT(i, v) do { } while (0)
+#define SEC_SUM(i, v) do { } while (0)
 #define SEC_MARK(k) do { } while (0)
 #endif
     for (;;) {
@@ -365,6 +453,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
             asm volatile("" : : "v"(a0), "v"(a1), "v"(a2), "v"(a3));
         }
+#endif
+#if RT_DEFER_FOLD
+        if (EXACT && __any(deferred)) {
+            if (deferred) start_deferred();
+        } else
 #endif
         if (EXACT && __any(dleft != 0u)) {
             if (dleft != 0u) {
@@ -589,11 +682,28 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     // nothing to fold or park: resample_kernel writes this sample's slot
                 } else if (EXACT) {
 #if RT_SECTIONS
-                    if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(7, 1);
+                    SEC_COUNT(9, __ballot(dleft != 0u) != 0 ? 1u : 0u);
+                    SEC_COUNT(10, (uint32_t)__popcll(__ballot(dleft != 0u)));
 #endif
-                    drain_all(dleft);   // the previous sample's fold completes first
                     const uint32_t m = (uint32_t)(fold_top + 1);
                     const uint32_t base = lsu(VS_BASE);
+#if RT_DEFER_FOLD
+                    // every sample has its own parked slot, so folds may complete in any order: a sample
+                    // without levels completes at once, and a fold that would wait for the previous one
+                    // is only recorded here (L in VS_LD, its level count in VS_PCOS; both are free until
+                    // the next path's first vertex) and started at the top of the next iteration, whose
+                    // loads follow no store of that iteration
+                    if (m != 0u && dleft != 0u) {
+                        st3(VS_LD, L);
+                        lsu(VS_PCOS) = m;
+                        uint32_t nb = base + m;
+                        if (nb >= Q.stack_depth) nb -= Q.stack_depth;
+                        lsu(VS_BASE) = nb;
+                        deferred = true;
+                    } else
+#else
+                    drain_all(dleft);   // the previous sample's fold completes first
+#endif
                     if (m == 0u) {
                         complete(L, local, fidx);
                     } else {
@@ -650,17 +760,21 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         }
 
         if (!__any(have_pixel || alive)) {
+#if RT_DEFER_FOLD
+            if (EXACT && deferred) start_deferred();
+#endif
             if (EXACT) drain_all(dleft);
             break;
         }
 
         SEC_MARK(5);
 #if RT_SECTIONS
-        SEC_COUNT(0, 1);
-        SEC_COUNT(1, __popcll(__ballot(in_path)));
-        SEC_COUNT(2, __popcll(__ballot(dbg_vertex)));
-        SEC_COUNT(3, __popcll(__ballot(dbg_fin)));
-        SEC_COUNT(4, __popcll(__ballot(dbg_cam)));
+        SEC_COUNT(0, 1u);
+        SEC_COUNT(1, (uint32_t)__popcll(__ballot(in_path)));
+        SEC_COUNT(2, (uint32_t)__popcll(__ballot(dbg_vertex)));
+        SEC_COUNT(3, (uint32_t)__popcll(__ballot(dbg_fin)));
+        SEC_COUNT(4, (uint32_t)__popcll(__ballot(dbg_cam)));
+        SEC_COUNT(11, (uint32_t)__popcll(__ballot(dleft != 0u)));
         dbg_vertex = dbg_fin = dbg_cam = false;
 #endif
         // ======================= trace both rays of every lane =======================
@@ -709,6 +823,17 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
         }
         SEC_MARK(6);
+#if RT_SECTIONS
+        {   // (lane, candidate) pairs of this trace step: total, ray A's, and 64-lane chunks if compacted
+            const uint32_t npair = (uint32_t)(__popcll(ca) + __popcll(cb));
+            sec_w[15] = 0u;
+            SEC_SUM(15, npair);
+            SEC_SUM(7, npair);
+            SEC_SUM(13, (uint32_t)__popcll(ca));
+            const uint32_t tot = sec_w[15];
+            SEC_COUNT(8, (tot + 63u) >> 6);
+        }
+#endif
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
         auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
@@ -745,11 +870,133 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 }
                 tri = nt; useA = nuse; a = na; e1 = ne1; e2 = ne2;
             }
+#elif RT_MT_X2 == 2
+            // ray A's candidates, then ray B's, two per iteration in packed halves with the ray's own
+            // direction in both halves (a splat: no per-half select)
+            auto x2_loop = [&](uint64_t& cm, const V3 d, const bool isA) {
+                while (cm != 0) {
+                    // splats built inside the loop (the opaque copies keep LICM from hoisting 12 live
+                    // registers out of it)
+                    float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
+                    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
+                    const P3 Dv{f2{dx, dx}, f2{dy, dy}, f2{dz, dz}};
+#if RT_SECTIONS
+                    SEC_COUNT(5, 1u);
+                    SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+                    SEC_COUNT(12, isA ? (uint32_t)__popcll(__ballot(1)) : 0u);
+#endif
+                    const int tri0 = __builtin_ctzll(cm);
+                    cm &= cm - 1;
+                    const bool has1 = cm != 0;
+                    const int tri1 = has1 ? __builtin_ctzll(cm) : tri0;
+                    cm &= cm - 1;
+                    const float4* T0 = S.tris + 4 * tri0;
+                    const float4* T1 = S.tris + 4 * tri1;
+                    const float4 u0 = T0[0], w0 = T1[0];
+                    const P3 Sv = psub(P3{f2{ox, ox}, f2{oy, oy}, f2{oz, oz}}, P3{f2{u0.x, w0.x}, f2{u0.y, w0.y}, f2{u0.z, w0.z}});
+                    RT_SCHED_BARRIER();
+                    const float4 u1 = T0[1], w1 = T1[1];
+                    const P3 E1{f2{u1.x, w1.x}, f2{u1.y, w1.y}, f2{u1.z, w1.z}};
+                    const P3 S2 = pcross(Sv, E1);
+                    RT_SCHED_BARRIER();
+                    const float4 u2 = T0[2], w2 = T1[2];
+                    const P3 E2{f2{u2.x, w2.x}, f2{u2.y, w2.y}, f2{u2.z, w2.z}};
+                    const P3 S1 = pcross(Dv, E2);
+                    const f2 den = pdot(S1, E1), tn = pdot(S2, E2), b2n = pdot(S1, Sv), b3n = pdot(S2, Dv);
+                    double t;
+                    if (mt_screen(den.x, tn.x, b2n.x, b3n.x) && mt_tail(den.x, tn.x, b2n.x, b3n.x, t)) {
+                        if (isA) {
+                            if (t <= tA) { tA = t; triA = tri0; }
+                        } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                            occB = true;
+                            cm = 0;
+                        }
+                    }
+                    if (has1 && mt_screen(den.y, tn.y, b2n.y, b3n.y) && mt_tail(den.y, tn.y, b2n.y, b3n.y, t)) {
+                        if (isA) {
+                            if (t <= tA) { tA = t; triA = tri1; }
+                        } else if (!((double)slen < t + (double)0.01f)) {
+                            occB = true;
+                            cm = 0;
+                        }
+                    }
+                }
+            };
+            x2_loop(ca, dA, true);
+            x2_loop(cb, dB, false);
+#elif RT_MT_X2
+            // two candidates per iteration, in the halves of packed registers (rt_device.h mt_pre_x2):
+            // a lane with c candidates loops ceil(c / 2) times.  Results are applied in candidate order
+            // (first, then second), so ray A's closest hit keeps the later-leaf tie rule.
+            while ((ca | cb) != 0) {
+#if RT_SECTIONS
+                SEC_COUNT(5, 1u);
+                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+                SEC_COUNT(12, (uint32_t)__popcll(__ballot(ca != 0)));
+#endif
+                const bool useA0 = ca != 0;
+                uint64_t cur = useA0 ? ca : cb;
+                const int tri0 = __builtin_ctzll(cur);
+                if (useA0) ca = cur & (cur - 1);
+                else cb = cur & (cur - 1);
+                const bool has1 = (ca | cb) != 0;
+                const bool useA1 = ca != 0;
+                cur = useA1 ? ca : cb;
+                const int tri1 = has1 ? __builtin_ctzll(cur) : tri0;
+                if (has1) {
+                    if (useA1) ca = cur & (cur - 1);
+                    else cb = cur & (cur - 1);
+                }
+                // staged (loads next to their use, scheduling barriers between the stages): the packed
+                // temporaries of both tests fit the 8-wave register budget
+                const float4* T0 = S.tris + 4 * tri0;
+                const float4* T1 = S.tris + 4 * tri1;
+                const float4 u0 = T0[0], w0 = T1[0];
+                const P3 Sv = psub(P3{f2{o.x, o.x}, f2{o.y, o.y}, f2{o.z, o.z}}, P3{f2{u0.x, w0.x}, f2{u0.y, w0.y}, f2{u0.z, w0.z}});
+                RT_SCHED_BARRIER();
+                const float4 u1 = T0[1], w1 = T1[1];
+                const P3 E1{f2{u1.x, w1.x}, f2{u1.y, w1.y}, f2{u1.z, w1.z}};
+                const P3 S2 = pcross(Sv, E1);
+                RT_SCHED_BARRIER();
+                const float4 u2 = T0[2], w2 = T1[2];
+                const P3 E2{f2{u2.x, w2.x}, f2{u2.y, w2.y}, f2{u2.z, w2.z}};
+                const V3 d0 = useA0 ? dA : dB, d1 = useA1 ? dA : dB;
+                const P3 Dv{f2{d0.x, d1.x}, f2{d0.y, d1.y}, f2{d0.z, d1.z}};
+                const P3 S1 = pcross(Dv, E2);
+                MtPre m;
+                m.den = pdot(S1, E1);
+                m.tn = pdot(S2, E2);
+                m.b2n = pdot(S1, Sv);
+                m.b3n = pdot(S2, Dv);
+                double t;
+                const bool h0 = mt_screen(m.den.x, m.tn.x, m.b2n.x, m.b3n.x) && mt_tail(m.den.x, m.tn.x, m.b2n.x, m.b3n.x, t);
+#if RT_SECTIONS
+                SEC_COUNT(14, (uint32_t)__popcll(__ballot(h0)));
+#endif
+                if (h0) {
+                    if (useA0) {
+                        if (t <= tA) { tA = t; triA = tri0; }
+                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                        occB = true;
+                        cb = 0;
+                    }
+                }
+                const bool h1 = has1 && mt_screen(m.den.y, m.tn.y, m.b2n.y, m.b3n.y) && mt_tail(m.den.y, m.tn.y, m.b2n.y, m.b3n.y, t);
+                if (h1) {
+                    if (useA1) {
+                        if (t <= tA) { tA = t; triA = tri1; }
+                    } else if (!((double)slen < t + (double)0.01f)) {
+                        occB = true;
+                        cb = 0;
+                    }
+                }
+            }
 #else
             while ((ca | cb) != 0) {
 #if RT_SECTIONS
-                SEC_COUNT(6, __popcll(__ballot(1)));
-                if (__lane_id() == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) SEC_COUNT(5, 1);
+                SEC_COUNT(5, 1u);
+                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+                SEC_COUNT(12, (uint32_t)__popcll(__ballot(ca != 0)));
 #endif
                 const bool useA = ca != 0;
                 const uint64_t cur = useA ? ca : cb;
@@ -759,7 +1006,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 const V3 d = useA ? dA : dB;
                 const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
                 double t;
-                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
+#if RT_SECTIONS
+                SEC_COUNT(14, (uint32_t)__popcll(__ballot(mh)));
+#endif
+                if (mh) {
                     if (useA) {
                         if (t <= tA) { tA = t; triA = tri; }
                     } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
@@ -839,12 +1090,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // wave cycles per section -> counters[16 + section] (one atomic per wave and section)
     if (__lane_id() == 0)
         for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long*)&P.counters[16 + i], (unsigned long long)sec_cyc[i]);
-    // wave-level counts live in the lane that counted them: reduce over the wave
-    for (int i = 0; i < 8; ++i) {
-        uint64_t v = sec_n[i];
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
-        if (__lane_id() == 0) atomicAdd((unsigned long long*)&P.counters[24 + i], (unsigned long long)v);
-    }
+    // the wave's event counts -> counters[24 + i]
+    if (lane < RT_SEC_COUNTS) atomicAdd((unsigned long long*)&P.counters[24 + lane], (unsigned long long)sec_w[lane]);
 #endif
 }
 

@@ -38,12 +38,17 @@ def main():
         names = ["service head", "vertex", "finish", "queue", "camera", "box loop", "moller-trumbore", "(entry)"]
         tot = float(sum(cyc)) or 1.0
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
-        n = c.debug_counters(32)[24:32]
+        n = c.debug_counters(40)[24:40]
         it = max(n[0], 1)
+        samples = args.width * args.height * args.spp
         print({"wave_iterations": n[0], "lanes_on_path/it": round(n[1] / it, 2), "vertex/it": round(n[2] / it, 2),
-               "finish/it": round(n[3] / it, 2), "camera/it": round(n[4] / it, 2), "mt_iters/it": round(n[5] / it, 2),
-               "mt_lane_util": round(n[6] / max(n[5], 1) / 64, 3), "fold_iters/it": round(n[7] / it, 2),
-               "iterations_per_sample_lane": round(n[0] * 64 / (args.width * args.height * args.spp), 3)})
+               "finish/it": round(n[3] / it, 2), "camera/it": round(n[4] / it, 2),
+               "mt_iters/it": round(n[5] / it, 2), "mt_lane_util": round(n[6] / max(n[5], 1) / 64, 3),
+               "pairs/it": round(n[7] / it, 2), "compacted_chunks/it": round(n[8] / it, 2),
+               "pairsA/it": round(n[13] / it, 2), "mt_lanesA/it": round(n[12] / it, 2), "mt_hits/it": round(n[14] / it, 2),
+               "fin_iters_with_drain/it": round(n[9] / it, 3), "fin_lanes_with_drain/it": round(n[10] / it, 3),
+               "drain_lanes_top/it": round(n[11] / it, 2),
+               "lane_iterations_per_sample": round(n[0] * 64 / samples, 3)})
     c.close()
 
 
