@@ -50,7 +50,8 @@ class Stats(C.Structure):
                 ("wave_tri_tests", C.c_uint64), ("wave_service", C.c_uint64), ("wave_fold", C.c_uint64),
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
                 ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
-                ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64)]
+                ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64),
+                ("pair_cap", C.c_uint32)]
 
 _DIAGNOSTIC = {"rt_debug_counters"}
 

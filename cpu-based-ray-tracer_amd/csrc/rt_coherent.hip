@@ -113,19 +113,20 @@ struct VertexRng {
 
 // the distinct leaf boxes, read with scalar loads (constant address space: wave-uniform index)
 typedef const __attribute__((address_space(4))) float cfloat;
+typedef float box8 __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) box8 cbox8;
 
 // AABB_3D::intersects_with_ray (MC/BoundingVolume.h:173-215) for a ray with a finite reciprocal
 // direction: per axis the near plane distance is min((lo - o) * rcp, (hi - o) * rcp) -- the
 // correctly rounded subtraction and multiplication are monotone, so the min is exactly the value of
 // the plane the reference selects by the direction's sign -- and no term can be NaN (rt_device.h
-// slab_hit_finite).  s0 = lo - o, s1 = hi - o.
-__device__ __forceinline__ bool box_hit(const V3& s0, const V3& s1, const V3& rc)
+// slab_hit_finite).  sx = (lo.x - o.x, hi.x - o.x), ... in the halves of packed registers: one
+// v_pk_mul_f32 per axis gives both plane distances, each rounded as the scalar product.
+__device__ __forceinline__ bool box_hit_pk(const f2 sx, const f2 sy, const f2 sz, const V3& rc)
 {
-    const float ax = s0.x * rc.x, bx = s1.x * rc.x;
-    const float ay = s0.y * rc.y, by = s1.y * rc.y;
-    const float az = s0.z * rc.z, bz = s1.z * rc.z;
-    const float tin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax, bx), __builtin_fminf(ay, by)), __builtin_fminf(az, bz));
-    const float tout = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax, bx), __builtin_fmaxf(ay, by)), __builtin_fmaxf(az, bz));
+    const f2 ax = sx * f2{rc.x, rc.x}, ay = sy * f2{rc.y, rc.y}, az = sz * f2{rc.z, rc.z};
+    const float tin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax.x, ax.y), __builtin_fminf(ay.x, ay.y)), __builtin_fminf(az.x, az.y));
+    const float tout = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax.x, ax.y), __builtin_fmaxf(ay.x, ay.y)), __builtin_fmaxf(az.x, az.y));
     return (tout >= 0.0f) && (tin <= tout);
 }
 
@@ -163,8 +164,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // [3] finishing lanes, [4] camera lanes, [5] MT loop wave iterations, [6] MT lanes tested,
 // [7] (lane, candidate) pairs, [8] 64-pair chunks if compacted, [9] finishing wave iterations with a
 // fold still draining, [10] lanes finishing with a fold still draining, [11] lanes draining at the top,
-// [12] MT lanes on ray A, [13] ray A pairs, [14] MT hits (fp64 part passed), [15] scratch
-#define RT_SEC_COUNTS 16
+// [12] MT lanes on ray A, [13] ray A pairs, [14] MT hits (fp64 part passed), [15] scratch, [16..18]
+// distinct candidate triangles of the wave (ray A, ray B, either)
+#define RT_SEC_COUNTS 20
 #ifndef RT_PAD_VALU
 #define RT_PAD_VALU 0
 #endif
@@ -173,30 +175,22 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BOX_UNROLL
 #define RT_BOX_UNROLL 4
 #endif
-// Moller-Trumbore loop: load the next candidate's triangle before testing the current one (A/B knob;
-// as written 14 VGPRs spill at 8 waves per SIMD: -6 %)
-#ifndef RT_MT_PREFETCH
-#define RT_MT_PREFETCH 0
-#endif
-// Moller-Trumbore loop: two candidates per iteration in packed f32 halves (A/B knob: 1 = A and B
-// candidates mixed, 2 = ray A's then ray B's with a splat direction).  At 8 waves per SIMD the packed
-// temporaries spill (2: 25 VGPRs): 5926 -> 5354 Msamples/s
-#ifndef RT_MT_X2
-#define RT_MT_X2 0
-#endif
-#ifndef RT_MT_X2_STAGED
-#define RT_MT_X2_STAGED 1
-#endif
-#if RT_MT_X2_STAGED
-#define RT_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define RT_SCHED_BARRIER() do { } while (0)
-#endif
 // a path that ends while the previous fold still drains: its fold starts at the top of the next
 // iteration (1) instead of completing the previous fold at once after the iteration's stores (0);
 // A/B: 5926 -> 5650 Msamples/s (slower, as the early drain)
 #ifndef RT_DEFER_FOLD
 #define RT_DEFER_FOLD 0
+#endif
+// NARROW Moller-Trumbore loop: the next candidate's triangle read from LDS one test ahead (A/B knob)
+#ifndef RT_MT_PREFETCH
+#define RT_MT_PREFETCH 0
+#endif
+// Moller-Trumbore spread over the wave through an LDS (lane, candidate) pair list (A/B build; the host
+// sizes the list from RT_PAIR_CAP).  C4: 6209 -> 5294 Msamples/s (MT loop iterations 13.5 -> 5.6 per
+// trace step at 91 % lane use, but each chunk costs the list writes, 10 ds_bpermute and the hit
+// returns, and ray B loses its early exit)
+#ifndef RT_MT_COMPACT
+#define RT_MT_COMPACT 0
 #endif
 // fold levels drained per iteration at the top of the loop, their ring loads issued together: a fold
 // then rarely still drains when the next path ends (where completing it waits on loads issued after
@@ -237,7 +231,8 @@ struct GeneralSlab { static constexpr bool value = false; };
 // BVH = true: the scene in HBM (read through L2/MALL); the two rays of a lane walk the stackless BVH
 // one after the other (A, then B) in the megakernel's rounds of `steps` box tests with up to two
 // postponed leaves, and a lane is served once both of its rays are done.
-template <bool EXACT, bool BVH>
+// NARROW (leaf-box variant, <= 32 triangles): ray A's and ray B's candidates in the two halves of one mask.
+template <bool EXACT, bool BVH, bool NARROW>
 __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
@@ -248,19 +243,19 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     } else {
         // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris; the leaf boxes
         // are read with scalar loads)
-        const uint32_t nq = 2 * P.n_nodes, tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
-        float4* dn = lds_scene;
-        float4* dt = dn + nq;
+        // (tris | mats | lnodes | ltris; the BVH nodes stay in HBM -- only a ray with a non-finite
+        // reciprocal direction walks them -- and the leaf boxes are read with scalar loads)
+        const uint32_t tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
+        float4* dt = lds_scene;
         float4* dm = dt + tq;
         float4* dl = dm + mq;
         float4* dlt = dl + lq;
-        for (uint32_t i = threadIdx.x; i < nq; i += blockDim.x) dn[i] = P.nodes[i];
         for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[i] = P.tris[i];
         for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
         for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
         for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
         __syncthreads();
-        S.nodes = dn; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt; S.lboxes = nullptr;
+        S.nodes = P.nodes; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt; S.lboxes = nullptr;
     }
 
     const uint32_t lane = __lane_id();
@@ -272,6 +267,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     auto lsu = [&](uint32_t f) -> uint32_t& { return reinterpret_cast<uint32_t*>(lstate)[f * 256u + tib]; };
     auto ls3 = [&](uint32_t f) { return V3{lsf(f), lsf(f + 1), lsf(f + 2)}; };
     auto st3 = [&](uint32_t f, V3 v) { lsf(f) = v.x; lsf(f + 1) = v.y; lsf(f + 2) = v.z; };
+    // leaf-box variant: the wave's (lane, candidate) pair list after the lane state (P.pair_cap entries)
+    uint16_t* const plist = reinterpret_cast<uint16_t*>(lstate + (P.has_light ? (EXACT ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256u) +
+                            (threadIdx.x >> 6) * P.pair_cap;
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
     // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
     // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
@@ -638,7 +636,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                         st3(VS_LD, divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2),
                                         (1.0f / Q.light_area)));
-                        dB = wl; rB = rcp3(wl);
+                        dB = wl; if (BVH) rB = rcp3(wl);
                         hasB = true;
                     }
                     // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
@@ -647,7 +645,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const V3 wi = glm_normalize(sample_hemisphere(n, G));
                         lsf(VS_PCOS) = dot(wi, n);
                         lsu(VS_MAT) = (uint32_t)mat;
-                        dA = wi; rA = rcp3(wi);
+                        dA = wi; if (BVH) rA = rcp3(wi);
                     }
                 };
                 if (Q.has_light) {
@@ -747,7 +745,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
             dA = w_normalize(V3{wd[0], wd[1], wd[2]});
-            rA = rcp3(dA);
+            if (BVH) rA = rcp3(dA);
             hasA = true; hasB = false;
             depth = 0;
             pend = false;
@@ -781,30 +779,50 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         if (!BVH) {
         const bool trA = in_path && hasA, trB = in_path && hasB;
         tA = 1.7976931348623157e308; triA = -1; occB = false;
+        // the reciprocal directions are computed here, not when the rays are set up: they are then
+        // temporaries of the box loop instead of 6 registers live across the iteration
+        rA = rcp3(dA); rB = rcp3(dB);
         const bool fin = (!trA || finite3(rA)) && (!trB || finite3(rB)) && kargs4().force_walk == 0u;
+        // candidate triangles (leaf-box masks): NARROW (<= 32 triangles) keeps ray A's in the low and
+        // ray B's in the high half of one mask, so the Moller-Trumbore loop walks one mask in DFS order
+        // (A first) without selecting between two
         uint64_t ca = 0, cb = 0;
+        uint32_t ma = 0, mb = 0;
         for (int rep = 0; rep < RT_REP_BOX; ++rep) {   // RT_REP_BOX > 1: cost-attribution builds only
-            if (RT_REP_BOX > 1) { ca = cb = 0; asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z)); }
-            cfloat* bx = (cfloat*)kargs4().lboxes;
+            if (RT_REP_BOX > 1) { ca = cb = 0; ma = mb = 0; asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z)); }
+            // a box is one 32-byte scalar load (s_load_dwordx8; a group of RT_BOX_UNROLL boxes waits once)
+            cbox8* bx = (cbox8*)kargs4().lboxes;
             const uint32_t nb = kargs4().n_lboxes;
-            auto one_box = [&](cfloat* q) {   // (lo.xyz, mask 0-31)(hi.xyz, mask 32-63), rt_layout.h
-                const V3 s0{q[0] - o.x, q[1] - o.y, q[2] - o.z}, s1{q[4] - o.x, q[5] - o.y, q[6] - o.z};
-                const uint64_t m = (uint64_t)(uint32_t)f2i(q[3]) | ((uint64_t)(uint32_t)f2i(q[7]) << 32);
-                if (box_hit(s0, s1, rA)) ca |= m;
-                if (box_hit(s0, s1, rB)) cb |= m;
+            auto one_box = [&](const box8 q) {   // (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, mask 0-31, mask 32-63), rt_layout.h
+                // (lo - o, hi - o) per axis in the halves of packed registers, shared by the two rays
+                const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
+                const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
+                const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
+                const bool hA = box_hit_pk(sx, sy, sz, rA), hB = box_hit_pk(sx, sy, sz, rB);
+                const uint32_t m0 = (uint32_t)f2i(q.s6);
+                if (NARROW) {
+                    ma |= hA ? m0 : 0u;
+                    mb |= hB ? m0 : 0u;
+                } else {
+                    const uint64_t m = (uint64_t)m0 | ((uint64_t)(uint32_t)f2i(q.s7) << 32);
+                    ca |= hA ? m : 0ull;
+                    cb |= hB ? m : 0ull;
+                }
             };
             uint32_t b = 0;
 #if RT_BOX_UNROLL > 1
-            // RT_BOX_UNROLL boxes per scalar load (one wait per group instead of one per box)
             for (; b + RT_BOX_UNROLL <= nb; b += RT_BOX_UNROLL) {
-                cfloat* q = bx + 8 * b;
+                box8 q[RT_BOX_UNROLL];
 #pragma unroll
-                for (int u = 0; u < RT_BOX_UNROLL; ++u) one_box(q + 8 * u);
+                for (int u = 0; u < RT_BOX_UNROLL; ++u) q[u] = bx[b + u];
+#pragma unroll
+                for (int u = 0; u < RT_BOX_UNROLL; ++u) one_box(q[u]);
             }
 #endif
-            for (; b < nb; ++b) one_box(bx + 8 * b);
-            if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb));
+            for (; b < nb; ++b) one_box(bx[b]);
+            if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb), "v"(ma), "v"(mb));
         }
+        if (NARROW) { ca = ma; cb = mb; }
         if (!trA || !fin) ca = 0;
         if (!trB || !fin) cb = 0;
         if (!fin && (trA || trB)) {
@@ -832,182 +850,29 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             SEC_SUM(13, (uint32_t)__popcll(ca));
             const uint32_t tot = sec_w[15];
             SEC_COUNT(8, (tot + 63u) >> 6);
+            // the wave's distinct candidate triangles: ray A's, ray B's, either
+            uint32_t ua = 0, ub = 0, uab = 0;
+            for (uint32_t t = 0; t < 64u; ++t) {
+                const bool a_ = __ballot(((ca >> t) & 1u) != 0u) != 0, b_ = __ballot(((cb >> t) & 1u) != 0u) != 0;
+                ua += a_ ? 1u : 0u; ub += b_ ? 1u : 0u; uab += (a_ || b_) ? 1u : 0u;
+            }
+            SEC_COUNT(16, ua);
+            SEC_COUNT(17, ub);
+            SEC_COUNT(18, uab);
         }
 #endif
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
         auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
-#if RT_MT_PREFETCH
-            // the next candidate's vertices are read from LDS before the current candidate is tested
-            auto take = [&](bool& useA) -> int {
-                useA = ca != 0;
-                const uint64_t cur = useA ? ca : cb;
-                if (useA) ca = cur & (cur - 1);
-                else cb = cur & (cur - 1);
-                return cur != 0 ? __builtin_ctzll(cur) : -1;
-            };
-            auto fetch = [&](int tri, V3& a, V3& e1, V3& e2) {
-                const float4* q = S.tris + 4 * (tri < 0 ? 0 : tri);
-                a = V3{q[0].x, q[0].y, q[0].z}; e1 = V3{q[1].x, q[1].y, q[1].z}; e2 = V3{q[2].x, q[2].y, q[2].z};
-            };
-            bool useA;
-            int tri = take(useA);
-            V3 a, e1, e2;
-            fetch(tri, a, e1, e2);
-            while (tri >= 0) {
-                bool nuse;
-                const int nt = take(nuse);
-                V3 na, ne1, ne2;
-                fetch(nt, na, ne1, ne2);
-                double t;
-                if (moller_trumbore_od(a, e1, e2, o, useA ? dA : dB, t)) {
-                    if (useA) {
-                        if (t <= tA) { tA = t; triA = tri; }
-                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                        occB = true;
-                        break;   // B's candidates come last: nothing else to test
-                    }
-                }
-                tri = nt; useA = nuse; a = na; e1 = ne1; e2 = ne2;
-            }
-#elif RT_MT_X2 == 2
-            // ray A's candidates, then ray B's, two per iteration in packed halves with the ray's own
-            // direction in both halves (a splat: no per-half select)
-            auto x2_loop = [&](uint64_t& cm, const V3 d, const bool isA) {
-                while (cm != 0) {
-                    // splats built inside the loop (the opaque copies keep LICM from hoisting 12 live
-                    // registers out of it)
-                    float ox = o.x, oy = o.y, oz = o.z, dx = d.x, dy = d.y, dz = d.z;
-                    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
-                    const P3 Dv{f2{dx, dx}, f2{dy, dy}, f2{dz, dz}};
-#if RT_SECTIONS
-                    SEC_COUNT(5, 1u);
-                    SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
-                    SEC_COUNT(12, isA ? (uint32_t)__popcll(__ballot(1)) : 0u);
-#endif
-                    const int tri0 = __builtin_ctzll(cm);
-                    cm &= cm - 1;
-                    const bool has1 = cm != 0;
-                    const int tri1 = has1 ? __builtin_ctzll(cm) : tri0;
-                    cm &= cm - 1;
-                    const float4* T0 = S.tris + 4 * tri0;
-                    const float4* T1 = S.tris + 4 * tri1;
-                    const float4 u0 = T0[0], w0 = T1[0];
-                    const P3 Sv = psub(P3{f2{ox, ox}, f2{oy, oy}, f2{oz, oz}}, P3{f2{u0.x, w0.x}, f2{u0.y, w0.y}, f2{u0.z, w0.z}});
-                    RT_SCHED_BARRIER();
-                    const float4 u1 = T0[1], w1 = T1[1];
-                    const P3 E1{f2{u1.x, w1.x}, f2{u1.y, w1.y}, f2{u1.z, w1.z}};
-                    const P3 S2 = pcross(Sv, E1);
-                    RT_SCHED_BARRIER();
-                    const float4 u2 = T0[2], w2 = T1[2];
-                    const P3 E2{f2{u2.x, w2.x}, f2{u2.y, w2.y}, f2{u2.z, w2.z}};
-                    const P3 S1 = pcross(Dv, E2);
-                    const f2 den = pdot(S1, E1), tn = pdot(S2, E2), b2n = pdot(S1, Sv), b3n = pdot(S2, Dv);
-                    double t;
-                    if (mt_screen(den.x, tn.x, b2n.x, b3n.x) && mt_tail(den.x, tn.x, b2n.x, b3n.x, t)) {
-                        if (isA) {
-                            if (t <= tA) { tA = t; triA = tri0; }
-                        } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                            occB = true;
-                            cm = 0;
-                        }
-                    }
-                    if (has1 && mt_screen(den.y, tn.y, b2n.y, b3n.y) && mt_tail(den.y, tn.y, b2n.y, b3n.y, t)) {
-                        if (isA) {
-                            if (t <= tA) { tA = t; triA = tri1; }
-                        } else if (!((double)slen < t + (double)0.01f)) {
-                            occB = true;
-                            cm = 0;
-                        }
-                    }
-                }
-            };
-            x2_loop(ca, dA, true);
-            x2_loop(cb, dB, false);
-#elif RT_MT_X2
-            // two candidates per iteration, in the halves of packed registers (rt_device.h mt_pre_x2):
-            // a lane with c candidates loops ceil(c / 2) times.  Results are applied in candidate order
-            // (first, then second), so ray A's closest hit keeps the later-leaf tie rule.
-            while ((ca | cb) != 0) {
-#if RT_SECTIONS
-                SEC_COUNT(5, 1u);
-                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
-                SEC_COUNT(12, (uint32_t)__popcll(__ballot(ca != 0)));
-#endif
-                const bool useA0 = ca != 0;
-                uint64_t cur = useA0 ? ca : cb;
-                const int tri0 = __builtin_ctzll(cur);
-                if (useA0) ca = cur & (cur - 1);
-                else cb = cur & (cur - 1);
-                const bool has1 = (ca | cb) != 0;
-                const bool useA1 = ca != 0;
-                cur = useA1 ? ca : cb;
-                const int tri1 = has1 ? __builtin_ctzll(cur) : tri0;
-                if (has1) {
-                    if (useA1) ca = cur & (cur - 1);
-                    else cb = cur & (cur - 1);
-                }
-                // staged (loads next to their use, scheduling barriers between the stages): the packed
-                // temporaries of both tests fit the 8-wave register budget
-                const float4* T0 = S.tris + 4 * tri0;
-                const float4* T1 = S.tris + 4 * tri1;
-                const float4 u0 = T0[0], w0 = T1[0];
-                const P3 Sv = psub(P3{f2{o.x, o.x}, f2{o.y, o.y}, f2{o.z, o.z}}, P3{f2{u0.x, w0.x}, f2{u0.y, w0.y}, f2{u0.z, w0.z}});
-                RT_SCHED_BARRIER();
-                const float4 u1 = T0[1], w1 = T1[1];
-                const P3 E1{f2{u1.x, w1.x}, f2{u1.y, w1.y}, f2{u1.z, w1.z}};
-                const P3 S2 = pcross(Sv, E1);
-                RT_SCHED_BARRIER();
-                const float4 u2 = T0[2], w2 = T1[2];
-                const P3 E2{f2{u2.x, w2.x}, f2{u2.y, w2.y}, f2{u2.z, w2.z}};
-                const V3 d0 = useA0 ? dA : dB, d1 = useA1 ? dA : dB;
-                const P3 Dv{f2{d0.x, d1.x}, f2{d0.y, d1.y}, f2{d0.z, d1.z}};
-                const P3 S1 = pcross(Dv, E2);
-                MtPre m;
-                m.den = pdot(S1, E1);
-                m.tn = pdot(S2, E2);
-                m.b2n = pdot(S1, Sv);
-                m.b3n = pdot(S2, Dv);
-                double t;
-                const bool h0 = mt_screen(m.den.x, m.tn.x, m.b2n.x, m.b3n.x) && mt_tail(m.den.x, m.tn.x, m.b2n.x, m.b3n.x, t);
-#if RT_SECTIONS
-                SEC_COUNT(14, (uint32_t)__popcll(__ballot(h0)));
-#endif
-                if (h0) {
-                    if (useA0) {
-                        if (t <= tA) { tA = t; triA = tri0; }
-                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                        occB = true;
-                        cb = 0;
-                    }
-                }
-                const bool h1 = has1 && mt_screen(m.den.y, m.tn.y, m.b2n.y, m.b3n.y) && mt_tail(m.den.y, m.tn.y, m.b2n.y, m.b3n.y, t);
-                if (h1) {
-                    if (useA1) {
-                        if (t <= tA) { tA = t; triA = tri1; }
-                    } else if (!((double)slen < t + (double)0.01f)) {
-                        occB = true;
-                        cb = 0;
-                    }
-                }
-            }
-#else
-            while ((ca | cb) != 0) {
-#if RT_SECTIONS
-                SEC_COUNT(5, 1u);
-                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
-                SEC_COUNT(12, (uint32_t)__popcll(__ballot(ca != 0)));
-#endif
-                const bool useA = ca != 0;
-                const uint64_t cur = useA ? ca : cb;
-                const int tri = __builtin_ctzll(cur);
-                if (useA) ca = cur & (cur - 1);
-                else cb = cur & (cur - 1);
+            auto test = [&](const bool useA, const int tri, uint64_t& rest) {
                 const V3 d = useA ? dA : dB;
                 const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
                 double t;
                 const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
 #if RT_SECTIONS
+                SEC_COUNT(5, 1u);
+                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+                SEC_COUNT(12, (uint32_t)__popcll(__ballot(useA)));
                 SEC_COUNT(14, (uint32_t)__popcll(__ballot(mh)));
 #endif
                 if (mh) {
@@ -1015,11 +880,55 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         if (t <= tA) { tA = t; triA = tri; }
                     } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                         occB = true;
-                        cb = 0;
+                        rest = 0;   // B's candidates come last: nothing else to test
                     }
                 }
+            };
+            if (NARROW && RT_MT_PREFETCH) {
+                // the next candidate's triangle is read from LDS before the current one is tested
+                uint64_t cm = ca | (cb << 32);
+                if (cm != 0) {
+                    uint32_t bit = (uint32_t)__builtin_ctzll(cm);
+                    cm &= cm - 1;
+                    const float4* T = S.tris + 4 * (bit & 31u);
+                    float4 u0 = T[0], u1 = T[1], u2 = T[2];
+                    for (;;) {
+                        const uint32_t nbit = cm != 0 ? (uint32_t)__builtin_ctzll(cm) : bit;
+                        const float4* N = S.tris + 4 * (nbit & 31u);
+                        const float4 n0 = N[0], n1 = N[1], n2 = N[2];
+                        const bool useA = bit < 32u;
+                        double t;
+                        const bool mh = moller_trumbore_od(V3{u0.x, u0.y, u0.z}, V3{u1.x, u1.y, u1.z}, V3{u2.x, u2.y, u2.z}, o, useA ? dA : dB, t);
+                        if (mh) {
+                            if (useA) {
+                                if (t <= tA) { tA = t; triA = (int)(bit & 31u); }
+                            } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                                occB = true;
+                                cm = 0;
+                            }
+                        }
+                        if (cm == 0) break;
+                        cm &= cm - 1;
+                        bit = nbit; u0 = n0; u1 = n1; u2 = n2;
+                    }
+                }
+            } else if (NARROW) {
+                uint64_t cm = ca | (cb << 32);
+                while (cm != 0) {
+                    const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
+                    cm &= cm - 1;
+                    test(bit < 32u, (int)(bit & 31u), cm);
+                }
+            } else {
+                while ((ca | cb) != 0) {
+                    const bool useA = ca != 0;
+                    const uint64_t cur = useA ? ca : cb;
+                    const int tri = __builtin_ctzll(cur);
+                    if (useA) ca = cur & (cur - 1);
+                    else cb = cur & (cur - 1);
+                    test(useA, tri, cb);
+                }
             }
-#endif
         };
         for (int rep = 1; rep < RT_REP_MT; ++rep) {   // cost-attribution builds only: results discarded
             uint64_t xa = ca, xb = cb;
@@ -1028,7 +937,82 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             mt_loop(xa, xb, xt, xtri, xo);
             asm volatile("" : : "v"(xt), "v"(xtri), "v"(xo));
         }
-        mt_loop(ca, cb, tA, triA, occB);
+        if (RT_MT_COMPACT && kargs4().pair_cap != 0u) {
+            // Moller-Trumbore spread over the wave (A/B build RT_MT_COMPACT=1 + RT_PAIR_CAP; slower than the per-lane loop:
+            // DESIGN.md 6.1).  The lanes' (lane, candidate) pairs -- ray A's candidates, then ray B's, in
+            // DFS order -- are listed in LDS at the lane's exclusive prefix sum of pair counts; each
+            // 64-pair chunk runs one test per lane on the owner's ray (fetched with ds_bpermute), and the
+            // results return to their owners: a blocking ray-B hit by ballot over the owner's positions,
+            // ray-A hits in position (= DFS) order with the reference's `t <= tA` update
+            // (MC/BVH.h:97-100), so the closest hit and its tie rule are unchanged.
+            CKParams& Q = kargs4();
+            const uint32_t cap = Q.pair_cap;
+            const uint32_t nA = (uint32_t)__popcll(ca), n = nA + (uint32_t)__popcll(cb);
+            const uint32_t excl = wave_incl_scan(n) - n;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + n), 63);
+            for (uint32_t w0 = 0; w0 < total; w0 += cap) {
+                const uint32_t wn = total - w0 < cap ? total - w0 : cap;
+                if (excl < w0 + wn && excl + n > w0) {
+                    // this lane's pairs inside the window: entry = owner lane | triangle << 6 | ray B << 12
+                    uint64_t a = ca, b = cb;
+                    uint32_t idx = excl;
+                    while ((a | b) != 0u && idx < w0 + wn) {
+                        const bool isA = a != 0u;
+                        const uint64_t cur = isA ? a : b;
+                        const uint32_t tri = (uint32_t)__builtin_ctzll(cur);
+                        if (isA) a = cur & (cur - 1u);
+                        else b = cur & (cur - 1u);
+                        if (idx >= w0) plist[idx - w0] = (uint16_t)(lane | (tri << 6) | (isA ? 0u : 4096u));
+                        ++idx;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (uint32_t c0 = 0; c0 < wn; c0 += 64u) {
+                    const uint32_t q = c0 + lane;
+                    const bool valid = q < wn;
+                    const uint32_t e = valid ? (uint32_t)plist[q] : 0u;
+                    const uint32_t own = e & 63u, tri = (e >> 6) & 63u;
+                    const bool isB = (e & 4096u) != 0u;
+                    // the owner's direction (A or B) and origin; both directions are fetched (every lane
+                    // takes part in a ds_bpermute) and selected per component
+                    V3 pd;
+                    pd.x = lane_f(own, dA.x); { const float v = lane_f(own, dB.x); pd.x = isB ? v : pd.x; }
+                    pd.y = lane_f(own, dA.y); { const float v = lane_f(own, dB.y); pd.y = isB ? v : pd.y; }
+                    pd.z = lane_f(own, dA.z); { const float v = lane_f(own, dB.z); pd.z = isB ? v : pd.z; }
+                    const V3 po{lane_f(own, o.x), lane_f(own, o.y), lane_f(own, o.z)};
+                    const float psl = lane_f(own, slen);
+                    double t = 0.0;
+                    bool hit = false;
+                    if (valid) {
+                        const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
+                        hit = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, po, pd, t);
+                    }
+                    // this lane's pairs in the chunk: positions [s, s + n)
+                    const int s0 = (int)excl - (int)(w0 + c0);
+                    const int lo = s0 < 0 ? 0 : (s0 > 64 ? 64 : s0);
+                    const int hiA = s0 + (int)nA < 0 ? 0 : (s0 + (int)nA > 64 ? 64 : s0 + (int)nA);
+                    const int hi = s0 + (int)n < 0 ? 0 : (s0 + (int)n > 64 ? 64 : s0 + (int)n);
+                    // ray B: any blocking hit occludes (MC/Renderer.cpp:184)
+                    const uint64_t blk = __ballot(hit && isB && !((double)psl < t + (double)0.01f));
+                    if ((blk & bit_range(lo, hi)) != 0u) occB = true;
+                    // ray A: hits in position order, t <= tA (the later leaf wins a tie)
+                    uint64_t mine = __ballot(hit && !isB) & bit_range(lo, hiA);
+                    while (__any(mine != 0u)) {
+                        const uint32_t src = mine != 0u ? (uint32_t)__builtin_ctzll(mine) : lane;
+                        const uint32_t tlo = lane_u(src, (uint32_t)__double2loint(t)), thi = lane_u(src, (uint32_t)__double2hiint(t));
+                        const uint32_t htri = lane_u(src, tri);
+                        if (mine != 0u) {
+                            const double ht = __hiloint2double((int)thi, (int)tlo);
+                            if (ht <= tA) { tA = ht; triA = (int)htri; }
+                            mine &= mine - 1u;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+        } else {
+            mt_loop(ca, cb, tA, triA, occB);
+        }
         } else {
             // BVH rounds (the megakernel's, rt_kernels.hip): `steps` box tests per round on the lane's
             // current ray (A until it is done, then B), up to two leaves postponed in DFS order and
@@ -1095,10 +1079,12 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
 }
 
-template __global__ void pt_coherent_kernel<true, false>(KParams);
-template __global__ void pt_coherent_kernel<false, false>(KParams);
-template __global__ void pt_coherent_kernel<true, true>(KParams);
-template __global__ void pt_coherent_kernel<false, true>(KParams);
+template __global__ void pt_coherent_kernel<true, false, true>(KParams);
+template __global__ void pt_coherent_kernel<false, false, true>(KParams);
+template __global__ void pt_coherent_kernel<true, false, false>(KParams);
+template __global__ void pt_coherent_kernel<false, false, false>(KParams);
+template __global__ void pt_coherent_kernel<true, true, false>(KParams);
+template __global__ void pt_coherent_kernel<false, true, false>(KParams);
 
 // ---------------------------------------------------------------------------------------------
 // device checks of the primitives the kernels shortcut (C-ABI rt_debug_primitives): the reference's
@@ -1107,9 +1093,9 @@ template __global__ void pt_coherent_kernel<false, true>(KParams);
 //     -- Whitted::RayTriangleIntersection, MC/TriangleMesh.h:19-45 -- on (a, b, c, o, d): E1 = b - a,
 //     E2 = c - a as the scene builder stores them;
 //   * AABB_3D::intersects_with_ray (MC/BoundingVolume.h:173-215) in the three forms the kernels use:
-//     slab_hit (std::max/min NaN rules), slab_hit_finite (IEEE max3/min3) and this file's box_hit
-//     (leaf boxes of the vertex kernel); the last two only for a finite reciprocal direction, where the
-//     kernels use them (-1 otherwise).
+//     slab_hit (std::max/min NaN rules), slab_hit_finite (IEEE max3/min3) and this file's box_hit_pk
+//     (leaf boxes of the vertex kernel, packed products); the last two only for a finite reciprocal
+//     direction, where the kernels use them (-1 otherwise).
 __global__ void __launch_bounds__(256) debug_primitives_kernel(uint32_t n_mt, const float* __restrict__ mt, int32_t* __restrict__ mt_hit,
                                                                double* __restrict__ mt_t, uint32_t n_box, const float* __restrict__ box,
                                                                int32_t* __restrict__ box_out)
@@ -1128,9 +1114,9 @@ __global__ void __launch_bounds__(256) debug_primitives_kernel(uint32_t n_mt, co
         const Ray r = make_ray(V3{q[6], q[7], q[8]}, V3{q[9], q[10], q[11]});
         box_out[3 * i] = slab_hit(r, q[0], q[1], q[2], q[3], q[4], q[5]) ? 1 : 0;
         const bool fin = finite3(r.rcp);
-        const V3 s0{q[0] - r.o.x, q[1] - r.o.y, q[2] - r.o.z}, s1{q[3] - r.o.x, q[4] - r.o.y, q[5] - r.o.z};
+        const f2 sx = f2{q[0], q[3]} - f2{r.o.x, r.o.x}, sy = f2{q[1], q[4]} - f2{r.o.y, r.o.y}, sz = f2{q[2], q[5]} - f2{r.o.z, r.o.z};
         box_out[3 * i + 1] = fin ? (slab_hit_finite(r, q[0], q[1], q[2], q[3], q[4], q[5]) ? 1 : 0) : -1;
-        box_out[3 * i + 2] = fin ? (box_hit(s0, s1, r.rcp) ? 1 : 0) : -1;
+        box_out[3 * i + 2] = fin ? (box_hit_pk(sx, sy, sz, r.rcp) ? 1 : 0) : -1;
     }
 }
 
@@ -1150,12 +1136,16 @@ size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit)
 
 hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
 {
+    const bool narrow = !bvh && P.n_tris <= 32;
     if (bvh) {
-        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true>), dim3(grid), dim3(block), lds, stream, P);
-        else hipLaunchKernelGGL((pt_coherent_kernel<false, true>), dim3(grid), dim3(block), lds, stream, P);
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true, false>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, true, false>), dim3(grid), dim3(block), lds, stream, P);
+    } else if (narrow) {
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, true>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, true>), dim3(grid), dim3(block), lds, stream, P);
     } else {
-        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false>), dim3(grid), dim3(block), lds, stream, P);
-        else hipLaunchKernelGGL((pt_coherent_kernel<false, false>), dim3(grid), dim3(block), lds, stream, P);
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, false>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, false>), dim3(grid), dim3(block), lds, stream, P);
     }
     return hipGetLastError();
 }
@@ -1164,9 +1154,9 @@ int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes)
 {
     int n = 0;
     hipError_t e;
-    if (bvh) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true>, block, lds_bytes)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true>, block, lds_bytes);
-    else e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, false>, block, lds_bytes)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, false>, block, lds_bytes);
+    if (bvh) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true, false>, block, lds_bytes)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true, false>, block, lds_bytes);
+    else e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, false, false>, block, lds_bytes)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, false, false>, block, lds_bytes);
     return e == hipSuccess ? n : 0;
 }

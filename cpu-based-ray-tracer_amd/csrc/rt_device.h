@@ -192,44 +192,34 @@ __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const
     return moller_trumbore_od(a, e1, e2, r.o, r.d, t_out);
 }
 
-// ------------------------------------------------------------------------------ two tests per lane
-// Two Moller-Trumbore tests (two triangles, or one triangle against two directions) of one origin in
-// the two halves of packed f32 registers: v_pk_mul_f32 / v_pk_add_f32 round each half exactly like
-// the scalar instruction, so every float is the one moller_trumbore_od computes, at half the issue
-// cost.  The double tail then runs per half.
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct P3 { f2 x, y, z; };
-__device__ __forceinline__ P3 psub(P3 a, P3 b) { return P3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ P3 pcross(P3 x, P3 y) { return P3{x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
-__device__ __forceinline__ f2 pdot(P3 a, P3 b) { const f2 tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return (tx + ty) + tz; }
+// ------------------------------------------------------------------------------ wave-level helpers
+// inclusive prefix sum over the 64 lanes of a wave (every lane active): row shifts 1, 2, 4, 8 within
+// each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals (GFX9 DPP)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// the value of `v` in lane `src` (every lane active; ds_bpermute_b32)
+__device__ __forceinline__ float lane_f(uint32_t src, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(v))); }
+__device__ __forceinline__ uint32_t lane_u(uint32_t src, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
+// bits [lo, hi) of a 64-bit mask, 0 <= lo <= hi <= 64
+__device__ __forceinline__ uint64_t bit_range(int lo, int hi)
+{
+    const uint64_t h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+    const uint64_t l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
+    return h & ~l;
+}
 
-// the float part: den, tn, b2n, b3n of both tests, and whether each survives the pre-screens
-struct MtPre { f2 den, tn, b2n, b3n; };
-__device__ __forceinline__ MtPre mt_pre_x2(const P3& a, const P3& e1, const P3& e2, const P3& o, const P3& d)
-{
-    const P3 S = psub(o, a);
-    const P3 S1 = pcross(d, e2), S2 = pcross(S, e1);
-    MtPre m;
-    m.den = pdot(S1, e1);
-    m.tn = pdot(S2, e2); m.b2n = pdot(S1, S); m.b3n = pdot(S2, d);
-    return m;
-}
-// the rest of moller_trumbore_od for one half (den, tn, b2n, b3n of that half)
-__device__ __forceinline__ bool mt_screen(float den, float tn, float b2n, float b3n)
-{
-    const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
-    const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
-    return (pos || ngt) && !((__builtin_fabsf(b2n) + __builtin_fabsf(b3n)) > __builtin_fabsf(den) * 1.00001f);
-}
-__device__ __forceinline__ bool mt_tail(float den, float tn, float b2n, float b3n, double& t_out)
-{
-    const double inv = rcp_f64_of_f32(den);
-    const double t = (double)tn * inv;
-    const double b2 = (double)b2n * inv;
-    const double b3 = (double)b3n * inv;
-    t_out = t;
-    return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
-}
+// ------------------------------------------------------------------------------ packed f32
+// two floats in the halves of a register pair: v_pk_mul_f32 / v_pk_add_f32 round each half exactly like
+// the scalar instruction, at half the issue cost
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 // cos/sin of the hemisphere angle phi = 2*PI*U in [0, 2*PI] (MC/WhittedMaterial.h:80-81 calls
 // std::cos/std::sin(float) -> glibc cosf/sinf).  Restatement of glibc 2.35's single-precision

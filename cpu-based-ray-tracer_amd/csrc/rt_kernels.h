@@ -43,6 +43,8 @@ struct KParams {
     uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
     uint32_t lds_pad;               // diagnostic: unused dynamic LDS bytes per workgroup (occupancy experiments)
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
+    uint32_t pair_cap;              // vertex kernel, leaf-box variant: (lane, candidate) pairs per wave in the LDS pair
+                                    // list after the lane state -- Moller-Trumbore spread over the wave (0: per-lane loop)
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray

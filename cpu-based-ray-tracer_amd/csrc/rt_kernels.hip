@@ -426,9 +426,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
             if (coherent && tracing) {
                 uint64_t cand = 0;
                 for (uint32_t b = 0; b < P.n_lboxes; ++b) {
-                    const float4 q0 = S.lboxes[2 * b], q1 = S.lboxes[2 * b + 1];
-                    if (slab_hit_finite(ray, q0.x, q0.y, q0.z, q1.x, q1.y, q1.z))
-                        cand |= (uint64_t)(uint32_t)f2i(q0.w) | ((uint64_t)(uint32_t)f2i(q1.w) << 32);
+                    const float4 q0 = S.lboxes[2 * b], q1 = S.lboxes[2 * b + 1];   // (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, masks)
+                    if (slab_hit_finite(ray, q0.x, q0.z, q1.x, q0.y, q0.w, q1.y))
+                        cand |= (uint64_t)(uint32_t)f2i(q1.z) | ((uint64_t)(uint32_t)f2i(q1.w) << 32);
                 }
                 while (cand != 0) {
                     const int tri = __builtin_ctzll(cand);

@@ -57,8 +57,10 @@ typedef struct {
     uint32_t n_lboxes;         // distinct leaf boxes of a small scene (<= 64 triangles), 0 otherwise
 } rt_scene_header;
 
-// lboxes (small scenes, the megakernel's coherent trace): 2 float4 per distinct leaf box,
-// (lo.xyz, bits of the mask of its triangles 0-31)(hi.xyz, bits of the mask of triangles 32-63)
+// lboxes (small scenes: the vertex kernel's leaf-box trace, the megakernel's coherent trace): 2 float4
+// per distinct leaf box, (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, bits of the mask of its triangles 0-31,
+// bits of the mask of triangles 32-63) -- each axis' planes adjacent, so a scalar load yields the
+// (lo, hi) pair of a packed subtraction
 #define RT_LBOX_QUADS 2
 
 #define RT_WENT_QUADS 4

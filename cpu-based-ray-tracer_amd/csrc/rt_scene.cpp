@@ -434,8 +434,9 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             for (size_t k = 0; k < uniq.size(); ++k) {
                 const Box& b = uniq[k].first;
                 float* q = &out.lboxes[8 * k];
-                q[0] = b.lo.x; q[1] = b.lo.y; q[2] = b.lo.z; q[3] = bits_as_float((int32_t)(uint32_t)uniq[k].second);
-                q[4] = b.hi.x; q[5] = b.hi.y; q[6] = b.hi.z; q[7] = bits_as_float((int32_t)(uint32_t)(uniq[k].second >> 32));
+                q[0] = b.lo.x; q[1] = b.hi.x; q[2] = b.lo.y; q[3] = b.hi.y;   // rt_layout.h: planes of an axis adjacent
+                q[4] = b.lo.z; q[5] = b.hi.z;
+                q[6] = bits_as_float((int32_t)(uint32_t)uniq[k].second); q[7] = bits_as_float((int32_t)(uint32_t)(uniq[k].second >> 32));
             }
         }
     }

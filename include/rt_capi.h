@@ -198,6 +198,8 @@ typedef struct {
     uint32_t kernel;          /* the path kernel of the last rt_render: RT_KERNEL_* */
     uint64_t resampled;       /* EXACT: samples whose path outgrew the fold ring, rendered again exactly */
     uint64_t overflow_lost;   /* EXACT: levels / samples that could not be kept (non-zero => RT_ERR_OVERFLOW) */
+    uint32_t pair_cap;        /* vertex kernel (leaf boxes): LDS pair-list entries per wave of the wave-spread
+                                 Moller-Trumbore; 0 = one lane tests its own candidates */
 } rt_stats;
 #define RT_KERNEL_MEGA 0      /* pt_megakernel (rt_kernels.hip): any scene, counters, G-buffer frames */
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */

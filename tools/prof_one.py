@@ -38,7 +38,7 @@ def main():
         names = ["service head", "vertex", "finish", "queue", "camera", "box loop", "moller-trumbore", "(entry)"]
         tot = float(sum(cyc)) or 1.0
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
-        n = c.debug_counters(40)[24:40]
+        n = c.debug_counters(44)[24:44]
         it = max(n[0], 1)
         samples = args.width * args.height * args.spp
         print({"wave_iterations": n[0], "lanes_on_path/it": round(n[1] / it, 2), "vertex/it": round(n[2] / it, 2),
@@ -48,6 +48,7 @@ def main():
                "pairsA/it": round(n[13] / it, 2), "mt_lanesA/it": round(n[12] / it, 2), "mt_hits/it": round(n[14] / it, 2),
                "fin_iters_with_drain/it": round(n[9] / it, 3), "fin_lanes_with_drain/it": round(n[10] / it, 3),
                "drain_lanes_top/it": round(n[11] / it, 2),
+               "union_tris_A/it": round(n[16] / it, 2), "union_tris_B/it": round(n[17] / it, 2), "union_tris_AB/it": round(n[18] / it, 2),
                "lane_iterations_per_sample": round(n[0] * 64 / samples, 3)})
     c.close()
 
