@@ -53,6 +53,10 @@ class Stats(C.Structure):
                 ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64),
                 ("pair_cap", C.c_uint32)]
 
+class GroupStats(C.Structure):
+    _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
+
+
 _DIAGNOSTIC = {"rt_debug_counters"}
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
@@ -136,6 +140,19 @@ def lib():
         "rt_render_denoised": (i32, [vp, C.POINTER(Camera), fp, fp, u32, u64, C.c_float, C.POINTER(DenoiseParams), C.POINTER(u32), fp]),
         "rt_denoise_restart": (i32, [vp]),
         "rt_get_gbuffer": (i32, [vp, fp, fp, fp, C.POINTER(i32), fp]),
+        "rt_group_create": (i32, [C.POINTER(vp), C.POINTER(i32), u32]),
+        "rt_group_destroy": (None, [vp]),
+        "rt_group_last_error": (C.c_char_p, [vp]),
+        "rt_group_size": (u32, [vp]),
+        "rt_group_member": (vp, [vp, u32]),
+        "rt_group_upload_scene": (i32, [vp, vp]),
+        "rt_group_resize": (i32, [vp, u32, u32, u32]),
+        "rt_group_render": (i32, [vp, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(u32)]),
+        "rt_group_frame_device": (i32, [vp, C.POINTER(vp)]),
+        "rt_group_read_accumulation": (i32, [vp, fp]),
+        "rt_group_reset_accumulation": (i32, [vp]),
+        "rt_group_synchronize": (i32, [vp]),
+        "rt_group_get_stats": (i32, [vp, C.POINTER(GroupStats)]),
     }
     for name, (res, args) in sig.items():
         if name in _DIAGNOSTIC and not hasattr(L, name):
@@ -371,6 +388,77 @@ def camera_default(W, H):
     if st != RT_OK:
         raise RtError(f"rt_camera_default failed {st}")
     return cam, proj, view
+
+
+class Group:
+    """Several GPUs rendering one frame (rt_group_*): member i renders the row bands b with b mod n == i on
+    devices[i]; the RGBA8 band sets are gathered to member 0 (RCCL for distinct devices, copies otherwise)."""
+
+    def __init__(self, devices):
+        self.h = C.c_void_p()
+        devs = (C.c_int32 * len(devices))(*devices)
+        st = lib().rt_group_create(C.byref(self.h), devs, len(devices))
+        if st != RT_OK:
+            raise RtError(f"rt_group_create failed with status {st}")
+        self.n = len(devices)
+        self.W = self.H = 0
+
+    def _check(self, st, what):
+        if st != RT_OK:
+            msg = lib().rt_group_last_error(self.h)
+            raise RtError(f"{what} failed ({st}): {msg.decode() if msg else ''}")
+
+    def upload(self, scene):
+        self._check(lib().rt_group_upload_scene(self.h, scene.h), "rt_group_upload_scene")
+
+    def resize(self, W, H, band=8):
+        self._check(lib().rt_group_resize(self.h, W, H, band), "rt_group_resize")
+        self.W, self.H = W, H
+
+    def render(self, cam, n_frames, first_frame=1, seed=0, rr=0.8, exact=True, fetch=True):
+        p = RenderParams(first_frame, n_frames, seed, rr, RENDER_EXACT if exact else 0)
+        if fetch:
+            rgba = np.zeros((self.H, self.W), np.uint32)
+            self._check(lib().rt_group_render(self.h, C.byref(cam), C.byref(p), rgba.ctypes.data_as(C.POINTER(C.c_uint32))), "rt_group_render")
+            return rgba
+        self._check(lib().rt_group_render(self.h, C.byref(cam), C.byref(p), None), "rt_group_render")
+        return None
+
+    def accumulation(self):
+        acc = np.zeros((self.H, self.W, 4), np.float32)
+        self._check(lib().rt_group_read_accumulation(self.h, _fp(acc)), "rt_group_read_accumulation")
+        return acc
+
+    def frame_device(self):
+        d = C.c_void_p()
+        self._check(lib().rt_group_frame_device(self.h, C.byref(d)), "rt_group_frame_device")
+        return d.value
+
+    def sync(self):
+        self._check(lib().rt_group_synchronize(self.h), "rt_group_synchronize")
+
+    def stats(self):
+        s = GroupStats()
+        self._check(lib().rt_group_get_stats(self.h, C.byref(s)), "rt_group_get_stats")
+        return s
+
+    def member_stats(self, i):
+        s = Stats()
+        m = lib().rt_group_member(self.h, i)
+        if lib().rt_get_stats(m, C.byref(s)) != RT_OK:
+            raise RtError("rt_get_stats failed")
+        return s
+
+    def close(self):
+        if self.h:
+            lib().rt_group_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:

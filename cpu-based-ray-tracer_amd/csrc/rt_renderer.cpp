@@ -157,15 +157,20 @@ rt::TriangleMesh::TriangleMesh(std::vector<float> raw_positions, const Material&
 // ============================================================================ Renderer
 void Renderer::check(rt_status s, const char* what) const
 {
-    if (s != RT_OK) throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
+    if (s != RT_OK)
+        throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + (group ? rt_group_last_error(group) : rt_last_error(ctx)));
 }
 
 Renderer::Renderer() : Renderer(Settings{}, true) {}
 
 Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
 {
-    rt_device_cfg cfg{settings.device, nullptr, 0};
-    check(rt_create(&ctx, &cfg), "rt_create");
+    if (settings.devices.size() > 1) {
+        check(rt_group_create(&group, settings.devices.data(), (uint32_t)settings.devices.size()), "rt_group_create");
+    } else {
+        rt_device_cfg cfg{settings.devices.empty() ? settings.device : settings.devices[0], nullptr, 0};
+        check(rt_create(&ctx, &cfg), "rt_create");
+    }
     if (cornell_box) {
         // Renderer::Renderer(): materials + six meshes + GenerateBVH (MC/Renderer.cpp:26-57)
         for (auto& m : rt::SceneBuilder::cornell_box_meshes()) {
@@ -179,7 +184,11 @@ Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
     }
 }
 
-Renderer::~Renderer() { rt_destroy(ctx); }
+Renderer::~Renderer()
+{
+    rt_group_destroy(group);
+    rt_destroy(ctx);
+}
 
 void Renderer::GenerateBVH()
 {
@@ -194,7 +203,7 @@ void Renderer::GenerateBVH()
         if (st != RT_OK) { rt_scene_destroy(sc); check(st, "rt_scene_add_mesh"); }
     }
     rt_status st = rt_scene_build(sc);
-    if (st == RT_OK) st = rt_upload_scene(ctx, sc);
+    if (st == RT_OK) st = group ? rt_group_upload_scene(group, sc) : rt_upload_scene(ctx, sc);
     rt_scene_destroy(sc);
     check(st, "GenerateBVH");
     bvh_dirty = false;
@@ -208,7 +217,8 @@ void Renderer::ResizeViewport(uint32_t width, uint32_t height)
     } else {
         frame_image_final = std::make_shared<rt::Image>(width, height);
     }
-    check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
+    if (group) check(rt_group_resize(group, width, height, settings.band), "rt_group_resize");
+    else check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
     frame_accumulating = 1;
 }
 
@@ -228,13 +238,19 @@ void Renderer::RenderFrames(const Camera& camera, uint32_t n)
         n = 1;
     }
     rt_render_params p{frame_accumulating, n, settings.seed + epoch, RR_survival_probability, settings.exact ? RT_RENDER_EXACT : 0u};
-    check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
+    if (group) check(rt_group_render(group, &cam, &p, frame_image_final->Data()), "rt_group_render");
+    else check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
     if (settings.accumulating) frame_accumulating += n;
     else frame_accumulating = 1;
 }
 
 const std::vector<float>& Renderer::GetAccumulation()
 {
+    if (group) {
+        accum_host.resize(frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0);
+        if (!accum_host.empty()) check(rt_group_read_accumulation(group, accum_host.data()), "rt_group_read_accumulation");
+        return accum_host;
+    }
     void* d_acc = nullptr;
     check(rt_device_buffers(ctx, &d_acc, nullptr), "rt_device_buffers");
     const size_t n = frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0;
@@ -248,6 +264,11 @@ const std::vector<float>& Renderer::GetAccumulation()
 
 float Renderer::LastKernelMilliseconds() const
 {
+    if (group) {   // the slowest member's band render
+        rt_group_stats gs{};
+        if (rt_group_get_stats(group, &gs) != RT_OK) return -1.0f;
+        return gs.max_member_kernel_ms;
+    }
     rt_stats st{};
     if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
     return st.last_kernel_ms;

@@ -10,6 +10,9 @@
 //                          accumulation (offline prototype color.h:33-51)
 //
 //   rt_render_ppm W H SPP out.ppm [--seed S] [--rr P] [--fast] [--per-frame] [--offline G] [--obj FILE R G B]...
+//                 [--devices 0,1,...] [--band ROWS]
+//   --devices: one frame on several GPUs (Renderer::Settings::devices -> rt_group_*: row bands per
+//              device, RGBA8 gathered to the first with RCCL); a device may repeat (bands on one GPU)
 //
 // The reference's other projects, through their drop-ins (include/rt/WhittedRenderer.h,
 // include/rt/DenoisingRenderer.h); SPP = frames:
@@ -174,7 +177,17 @@ int main(int argc, char** argv)
         else if (a == "--fast") s.exact = false;
         else if (a == "--per-frame") per_frame = true;
         else if (a == "--offline" && i + 1 < argc) gamma = std::strtod(argv[++i], nullptr);
-        else if (a == "--obj" && i + 4 < argc) {
+        else if (a == "--band" && i + 1 < argc) s.band = (uint32_t)std::atoi(argv[++i]);
+        else if (a == "--devices" && i + 1 < argc) {
+            const std::string list = argv[++i];
+            size_t at = 0;
+            while (at <= list.size()) {
+                const size_t comma = list.find(',', at);
+                s.devices.push_back(std::atoi(list.substr(at, comma == std::string::npos ? std::string::npos : comma - at).c_str()));
+                if (comma == std::string::npos) break;
+                at = comma + 1;
+            }
+        } else if (a == "--obj" && i + 4 < argc) {
             objs.push_back({argv[i + 1], std::strtof(argv[i + 2], nullptr), std::strtof(argv[i + 3], nullptr), std::strtof(argv[i + 4], nullptr)});
             i += 4;
         } else {
@@ -207,7 +220,8 @@ int main(int argc, char** argv)
             std::fprintf(stderr, "cannot write %s\n", out);
             return 1;
         }
-        std::printf("{\"width\": %u, \"height\": %u, \"spp\": %u, \"kernel_ms\": %.3f}\n", W, H, renderer.GetSPP(), renderer.LastKernelMilliseconds());
+        std::printf("{\"width\": %u, \"height\": %u, \"spp\": %u, \"kernel_ms\": %.3f, \"devices\": %zu}\n", W, H, renderer.GetSPP(),
+                    renderer.LastKernelMilliseconds(), s.devices.size() > 1 ? s.devices.size() : (size_t)1);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

@@ -70,6 +70,10 @@ public:
         uint64_t seed = 0;          // RNG key (frames are keyed by frame index; Reaccumulate bumps the epoch)
         bool exact = true;          // inner-first fold of the path recursion (bit-faithful accumulation)
         int device = 0;
+        // several GPUs for one frame (rt_group_*): row bands dealt over these devices, RGBA8 gathered to
+        // the first (RCCL when the devices are distinct); empty or one entry: a single device
+        std::vector<int> devices;
+        uint32_t band = 8;          // rows per band of the multi-GPU split
     };
 
     Renderer();                                  // Cornell box, device 0
@@ -102,6 +106,7 @@ private:
     uint32_t frame_accumulating = 1;
     uint64_t epoch = 0;
     rt_ctx* ctx = nullptr;
+    rt_group* group = nullptr;   // Settings::devices with more than one entry
     std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
     bool bvh_dirty = true;
 };

@@ -211,6 +211,43 @@ rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
  * stream synchronisation */
 rt_status rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
 
+/* ------------------------------------------------------------------ several GPUs, one frame
+ * A group of device contexts renders one frame together.  Replaces, across GPUs, the reference's
+ * std::execution::par row loop of Renderer::Render (MC/Renderer.cpp:100-110): member i (rank i of
+ * n) owns the row bands b with b mod n == i (bands of `band` rows, as rt_resize), renders them in one
+ * launch on its own device and stream, and the RGBA8 band sets are gathered to member 0 and reassembled
+ * into the full frame there.  The gather is RCCL (ncclGather over one communicator per member,
+ * ncclCommInitAll, issued as one group) when the member devices are distinct, device-to-device copies
+ * when a device repeats (RCCL takes one rank per GPU; e.g. n members on one GPU in tests) or when
+ * RT_GROUP_GATHER=copy.  Every pixel is the same as in a one-device render: the random stream is keyed by
+ * the global pixel. */
+typedef struct rt_group rt_group;
+rt_status rt_group_create(rt_group** out, const int32_t* devices, uint32_t n);
+void rt_group_destroy(rt_group* g);
+const char* rt_group_last_error(const rt_group* g);
+uint32_t rt_group_size(const rt_group* g);
+/* member i's context (rank i): stats, device buffers of its bands */
+rt_ctx* rt_group_member(rt_group* g, uint32_t i);
+rt_status rt_group_upload_scene(rt_group* g, const rt_scene* s);
+rt_status rt_group_resize(rt_group* g, uint32_t width, uint32_t height, uint32_t band);
+/* one Renderer::Render x n_frames on every member, then the gather.  Asynchronous unless out_rgba (width x
+ * height u32, ABGR, row 0 = bottom) is given; the members' overflow status is checked at the
+ * synchronisation (as rt_render) */
+rt_status rt_group_render(rt_group* g, const rt_camera* cam, const rt_render_params* p, uint32_t* out_rgba);
+/* the assembled RGBA8 frame on member 0's device (valid after rt_group_render's work completes) */
+rt_status rt_group_frame_device(rt_group* g, void** d_rgba);
+/* the accumulation (width x height x 4 f32, row 0 = bottom) gathered to the host */
+rt_status rt_group_read_accumulation(rt_group* g, float* out_accum);
+rt_status rt_group_reset_accumulation(rt_group* g);
+rt_status rt_group_synchronize(rt_group* g);
+typedef struct {
+    float last_ms;            /* the last rt_group_render: member 0's stream, first launch to assembled frame */
+    float max_member_kernel_ms; /* the slowest member's path-kernel time of that render */
+    uint32_t gather;          /* 1 = RCCL, 0 = device-to-device copies */
+    uint32_t n;               /* members */
+} rt_group_stats;
+rt_status rt_group_get_stats(rt_group* g, rt_group_stats* st);
+
 /* ------------------------------------------------------------------ the Denoiser (DN/ = Denoiser/8599RayTracerGUI/src/)
  * One call = one Renderer::Render of the Denoiser project (DN/Renderer.cpp:101-283): a 1-spp path-traced
  * frame through the pixel centres that records the G-buffer (DN/Renderer.cpp:285-311), the joint

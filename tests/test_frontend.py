@@ -55,6 +55,23 @@ def test_frontend_matches_golden(tmp_path, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("devices,band", [("0,0", "8"), ("0,0,0", "4")])
+def test_frontend_multi_device_matches_golden(tmp_path, devices, band):
+    """Renderer::Settings::devices (several GPUs, one frame through rt_group_*; here the members share
+    device 0): the reference's golden frame, per-frame loop and offline accumulation alike"""
+    out = tmp_path / "m.ppm"
+    r = subprocess.run([EXE, "64", "64", "16", str(out), "--devices", devices, "--band", band], check=True, capture_output=True, text=True)
+    assert f'"devices": {len(devices.split(","))}' in r.stdout
+    want, acc = golden_rgb(64, 64, 16)
+    assert np.array_equal(read_ppm(out), want)
+    out2 = tmp_path / "p.ppm"
+    subprocess.run([EXE, "64", "64", "16", str(out2), "--devices", devices, "--per-frame", "--offline", "2"], check=True, capture_output=True)
+    v = 255 * np.clip(np.power(acc[..., :3].astype(np.float64) / 16, 0.5), 0, 1)
+    want2 = np.where(v - np.floor(v) >= 0.5, np.floor(v) + 1, np.floor(v)).astype(np.int32)[::-1]
+    assert np.array_equal(read_ppm(out2), want2)
+
+
+@pytest.mark.gpu
 def test_frontend_offline_writer(tmp_path):
     out = tmp_path / "o.ppm"
     subprocess.run([EXE, "64", "64", "16", str(out), "--offline", "2"], check=True, capture_output=True)
