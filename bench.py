@@ -101,16 +101,26 @@ def host_cpu():
         core = read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id")
         if pkg is not None:
             pk.setdefault(pkg, set()).add(core)
-    usable = len(os.sched_getaffinity(0))
+    affinity = sorted(os.sched_getaffinity(0))
+    usable = len(affinity)
+    quota_cpus = None
     quota = read("/sys/fs/cgroup/cpu.max")
     if quota and quota.split()[0] != "max":
         q, per = quota.split()
-        usable = min(usable, max(1, int(int(q) / int(per))))
+        quota_cpus = max(1, int(int(q) / int(per)))
+        usable = min(usable, quota_cpus)
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if omp > 0:
         usable = min(usable, omp)
     per_socket = max((len(v) for v in pk.values()), default=usable)
-    return {"model": model, "sockets": len(pk) or 1, "physical_cores_per_socket": per_socket, "usable_cpus": usable}
+    # the physical cores the affinity mask spans (SMT siblings share one): with more of them than threads,
+    # the threads run one per physical core
+    phys = {(read(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id"), read(f"/sys/devices/system/cpu/cpu{c}/topology/core_id"))
+            for c in affinity}
+    smt = read("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list")
+    return {"model": model, "sockets": len(pk) or 1, "physical_cores_per_socket": per_socket, "usable_cpus": usable,
+            "affinity_cpus": len(affinity), "affinity_physical_cores": len(phys), "cgroup_quota_cpus": quota_cpus,
+            "omp_num_threads": omp or None, "cpu0_smt_siblings": smt}
 
 
 def cpu_baseline(W, H, seconds):
@@ -157,6 +167,7 @@ def cpu_baseline(W, H, seconds):
                 "rng": "shipped (thread_local mt19937 seed 5489, MSVC 32-bit distribution, persistent pool)",
                 "cpu_model": cpu["model"], "sockets": cpu["sockets"],
                 "physical_cores_per_socket": cpu["physical_cores_per_socket"],
+                "host": {k: cpu[k] for k in ("affinity_cpus", "affinity_physical_cores", "cgroup_quota_cpus", "omp_num_threads", "cpu0_smt_siblings")},
                 "socket_estimate": {"value": round(est, 2), "threads": cpu["physical_cores_per_socket"],
                                     "how": f"measured {per_thread:.4f} Msamples/s per thread at {threads} threads x "
                                            f"{cpu['physical_cores_per_socket']} physical cores of one socket (linear)"},

@@ -155,8 +155,9 @@ def lib():
         "rt_group_get_stats": (i32, [vp, C.POINTER(GroupStats)]),
     }
     for name, (res, args) in sig.items():
-        if name in _DIAGNOSTIC and not hasattr(L, name):
-            continue   # diagnostics only (A/B against older builds)
+        if (name in _DIAGNOSTIC or name.startswith("rt_group_")) and not hasattr(L, name):
+            continue   # diagnostics / multi-GPU entry points absent from an older A/B build (the product
+                       # library exports all: test_capi_cpu.test_library_exports_every_declared_symbol)
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -111,6 +111,20 @@ struct VertexRng {
     }
 };
 
+// one fold level from the ring: (direct term, cosine) and material -- with ring_pack the material is
+// the three sign bits of the direct term (one 16-byte load instead of two)
+__device__ __forceinline__ void ring_load(const CKParams& Q, size_t at, float4& e, int& m)
+{
+    e = Q.stack_ld[at];
+    if (Q.ring_pack) {
+        const uint32_t x = __float_as_uint(e.x), y = __float_as_uint(e.y), z = __float_as_uint(e.z);
+        m = (int)((x >> 31) | ((y >> 30) & 2u) | ((z >> 29) & 4u));
+        e = make_float4(__uint_as_float(x & 0x7FFFFFFFu), __uint_as_float(y & 0x7FFFFFFFu), __uint_as_float(z & 0x7FFFFFFFu), e.w);
+    } else {
+        m = Q.stack_mat[at];
+    }
+}
+
 // the distinct leaf boxes, read with scalar loads (constant address space: wave-uniform index)
 typedef const __attribute__((address_space(4))) float cfloat;
 typedef float box8 __attribute__((ext_vector_type(8)));
@@ -300,8 +314,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             for (uint32_t j = 0; j < RT_DRAIN_STEP; ++j) {
                 const uint32_t pj = pos >= j ? pos - j : pos + R - j;
                 const uint32_t at = j < dleft ? pj : pos;
-                e[j] = Q.stack_ld[RING_AT(at)];
-                m[j] = Q.stack_mat[RING_AT(at)];
+                ring_load(Q, RING_AT(at), e[j], m[j]);
             }
             V3 L = ls3(VS_DL);
 #pragma unroll
@@ -324,8 +337,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         }
 #endif
         const uint32_t pos = lsu(VS_DPOS);
-        const float4 e = Q.stack_ld[RING_AT(pos)];
-        const int m = Q.stack_mat[RING_AT(pos)];
+        float4 e;
+        int m;
+        ring_load(Q, RING_AT(pos), e, m);
         const float4 mb2 = S.mats[2 * m];
         const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
         const V3 L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(ls3(VS_DL), f), e.w), PDF), Q.rr));
@@ -354,8 +368,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
                 const uint32_t pj = pos >= j ? pos - j : pos + R - j;
                 const uint32_t at = j < dleft ? pj : pos;   // levels past the fold re-read the first one (unused)
-                e[j] = Q.stack_ld[RING_AT(at)];
-                m[j] = Q.stack_mat[RING_AT(at)];
+                ring_load(Q, RING_AT(at), e[j], m[j]);
             }
 #pragma unroll
             for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
@@ -538,7 +551,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             int mat = 0;
             bool emissive = false;
             if (hasA && triA >= 0) {
-                mat = f2i(S.tris[4 * triA].w);
+                mat = (BVH && kargs4().use_qnodes) ? f2i(kargs4().tabc[3 * triA].w) : f2i(S.tris[4 * triA].w);
                 emissive = S.mats[2 * mat].w != 0.0f;
             }
             bool vertex = false;
@@ -583,8 +596,16 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         fits = (pos + R - lo) % R >= dleft;
                     }
                     if (fits) {
-                        Q.stack_ld[RING_AT(pos)] = e;
-                        Q.stack_mat[RING_AT(pos)] = pm;
+                        if (Q.ring_pack) {
+                            // the material in the sign bits of the direct term (rt_kernels.h ring_pack)
+                            const float4 pe = make_float4(__uint_as_float((__float_as_uint(e.x) & 0x7FFFFFFFu) | ((pm & 1u) << 31)),
+                                                          __uint_as_float((__float_as_uint(e.y) & 0x7FFFFFFFu) | ((pm & 2u) << 30)),
+                                                          __uint_as_float((__float_as_uint(e.z) & 0x7FFFFFFFu) | ((pm & 4u) << 29)), e.w);
+                            Q.stack_ld[RING_AT(pos)] = pe;
+                        } else {
+                            Q.stack_ld[RING_AT(pos)] = e;
+                            Q.stack_mat[RING_AT(pos)] = pm;
+                        }
                         vertex = true;
                     } else {
                         // the path outgrew the ring: list the sample for the exact re-render
@@ -615,7 +636,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
-                const float4 tq3 = S.tris[4 * triA + 3];
+                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[triA] : S.tris[4 * triA + 3];
                 const V3 wo = neg(dA);
                 const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
                 const V3 N{tq3.x, tq3.y, tq3.z};
@@ -636,7 +657,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                         st3(VS_LD, divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2),
                                         (1.0f / Q.light_area)));
-                        dB = wl; if (BVH) rB = rcp3(wl);
+                        dB = wl;
                         hasB = true;
                     }
                     // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
@@ -645,7 +666,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const V3 wi = glm_normalize(sample_hemisphere(n, G));
                         lsf(VS_PCOS) = dot(wi, n);
                         lsu(VS_MAT) = (uint32_t)mat;
-                        dA = wi; if (BVH) rA = rcp3(wi);
+                        dA = wi;
                     }
                 };
                 if (Q.has_light) {
@@ -745,7 +766,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
             dA = w_normalize(V3{wd[0], wd[1], wd[2]});
-            if (BVH) rA = rcp3(dA);
             hasA = true; hasB = false;
             depth = 0;
             pend = false;
@@ -1028,11 +1048,37 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 if ((uint32_t)__popcll(act) <= thresh && srv != 0) break;
                 const bool curA = tiA < NN;
                 const V3 d = curA ? dA : dB;
-                const Ray r{o, d, curA ? rA : rB, d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
+                // the current ray's reciprocal direction, recomputed per round (not 6 registers live
+                // across the iteration)
+                const Ray r{o, d, rcp3(d), d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
                 const bool fin = __all(!tracing || finite3(r.rcp));
+                // compact BVH for an all-finite wave (rt_layout.h): quantized internal boxes (rounded
+                // outward: only extra visits), exact leaf boxes from the triangle's vertices
+                const bool qround = fin && Q.use_qnodes != 0u;
                 if (tracing) {
                     uint32_t ti = curA ? tiA : tiB;
                     int parked0 = -1, parked1 = -1;
+                    auto walk_q = [&]() {
+                        // every node's quantized box (16 B): an internal hit descends, a leaf hit parks the
+                        // triangle; its exact box is tested with its vertices at the end of the round
+                        const float ox = kargs4().q_origin[0], oy = kargs4().q_origin[1], oz = kargs4().q_origin[2];
+                        const float sx = kargs4().q_scale[0], sy = kargs4().q_scale[1], sz = kargs4().q_scale[2];
+                        const uint4* __restrict__ qn = kargs4().qnodes;
+                        for (uint32_t s = 0; s < steps && ti < NN; ++s) {
+                            const uint4 q = qn[ti];
+                            const float lx = __builtin_fmaf((float)(q.x & 0xFFFFu), sx, ox), hx = __builtin_fmaf((float)(q.x >> 16), sx, ox);
+                            const float ly = __builtin_fmaf((float)(q.y & 0xFFFFu), sy, oy), hy = __builtin_fmaf((float)(q.y >> 16), sy, oy);
+                            const float lz = __builtin_fmaf((float)(q.z & 0xFFFFu), sz, oz), hz = __builtin_fmaf((float)(q.z >> 16), sz, oz);
+                            const bool hit = slab_hit_finite(r, lx, ly, lz, hx, hy, hz);
+                            const bool leaf = (q.w & 0x80000000u) != 0u;
+                            ti = (hit && !leaf) ? ti + 1 : (leaf ? ti + 1 : q.w);
+                            if (hit && leaf) {
+                                const int tri = (int)(q.w & 0x7FFFFFFFu);
+                                if (parked0 < 0) parked0 = tri;
+                                else { parked1 = tri; break; }
+                            }
+                        }
+                    };
                     auto walk = [&](auto kind) {
                         for (uint32_t s = 0; s < steps && ti < NN; ++s) {
                             const float4 q0 = S.nodes[2 * ti];
@@ -1047,14 +1093,30 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                             }
                         }
                     };
-                    if (fin) walk(FiniteSlab{});
+                    if (qround) walk_q();
+                    else if (fin) walk(FiniteSlab{});
                     else walk(GeneralSlab{});
                     for (int slot = 0; slot < 2; ++slot) {
                         const int pk = slot == 0 ? parked0 : parked1;
                         if (pk < 0 || (!curA && occB)) continue;
-                        const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
+                        V3 va, e1, e2;
+                        if (qround) {
+                            const float4* ta = kargs4().tabc + 3 * pk;
+                            const float4 t0 = ta[0], t1 = ta[1], t2 = ta[2];
+                            // the exact leaf box: Triangle::Get3DAABB (MC/TriangleMesh.h:96-99)
+                            if (!slab_hit_finite(r, __builtin_fminf(__builtin_fminf(t0.x, t1.x), t2.x), __builtin_fminf(__builtin_fminf(t0.y, t1.y), t2.y),
+                                                 __builtin_fminf(__builtin_fminf(t0.z, t1.z), t2.z), __builtin_fmaxf(__builtin_fmaxf(t0.x, t1.x), t2.x),
+                                                 __builtin_fmaxf(__builtin_fmaxf(t0.y, t1.y), t2.y), __builtin_fmaxf(__builtin_fmaxf(t0.z, t1.z), t2.z)))
+                                continue;
+                            va = V3{t0.x, t0.y, t0.z};   // e1 = b - a, e2 = c - a: the floats `tris` holds
+                            e1 = sub(V3{t1.x, t1.y, t1.z}, va);
+                            e2 = sub(V3{t2.x, t2.y, t2.z}, va);
+                        } else {
+                            const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
+                            va = V3{t0.x, t0.y, t0.z}; e1 = V3{t1.x, t1.y, t1.z}; e2 = V3{t2.x, t2.y, t2.z};
+                        }
                         double t;
-                        if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                        if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {
                                 if (t <= tA) { tA = t; triA = pk; }   // the later leaf wins ties
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184

@@ -12,6 +12,10 @@ struct KParams {
     const float4* lnodes; uint32_t n_lnodes;
     const float4* ltris; uint32_t n_ltris;
     const float4* lboxes; uint32_t n_lboxes;   // small scenes: distinct leaf boxes + triangle masks (rt_layout.h)
+    // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex
+    // kernel's BVH variant walks it for waves whose rays all have a finite reciprocal direction
+    const uint4* qnodes; const float4* tabc; const float4* tnrm; uint32_t use_qnodes;
+    float q_origin[3], q_scale[3];
     float light_area; float light_emission[3]; int has_light;
     // Whitted shading (rt_whitted.hip): per-material (diffuse color, phong_diffuse), point lights, sky
     const float4* wmats; const float4* plights; uint32_t n_plights; float sky[3];
@@ -40,6 +44,10 @@ struct KParams {
     // scratch
     uint32_t* work_counter;
     float4* stack_ld; int32_t* stack_mat; uint32_t stack_depth; uint32_t total_threads;
+    // vertex kernel, EXACT: a scene of at most 8 materials keeps a fold level's material in the sign bits
+    // of its direct term (always +0 or positive; a zero's sign never reaches the accumulation: the sums
+    // start at +0), so a level is one float4 (stack_mat unused)
+    uint32_t ring_pack;
     uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
     uint32_t lds_pad;               // diagnostic: unused dynamic LDS bytes per workgroup (occupancy experiments)
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)

@@ -48,6 +48,8 @@ struct FlatScene {
     std::vector<float> nodes, tris, mats, lnodes, ltris, wmats, plights;   // float4-granular
     std::vector<float> went, wtris;                                       // Whitted world (C1)
     std::vector<float> lboxes;                                            // distinct leaf boxes (small scenes)
+    std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
+    std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag
     std::vector<float> dbg_node_f;    // 7 per node
     std::vector<int32_t> dbg_node_i;  // 5 per node

@@ -124,3 +124,22 @@ def test_full_frame_digest(ctx, fixture):
     rgba, acc = ctx.render(cam, 1, seed=0)
     assert hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest() == str(fixture["sha_accum_3840x2160_spp1_s0"])
     assert hashlib.sha256(np.ascontiguousarray(rgba).tobytes()).hexdigest() == str(fixture["sha_rgba_3840x2160_spp1_s0"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"}])
+def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):
+    """The vertex kernel's BVH variant (the C5 path) on the reference's 96x54x16 accumulation, with the
+    fold-level materials in their own array or in the direct term's sign bits, and walking the exact
+    nodes or the compact BVH (16-bit outward-rounded boxes, exact leaf boxes from the vertices)"""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    c = rt.Context(0)
+    c.upload(scene)
+    c.resize(96, 54)
+    cam, _, _ = rt.camera_default(96, 54)
+    rgba, acc = c.render(cam, 16, seed=0)
+    assert c.stats().kernel == 3   # RT_KERNEL_VERTEX_BVH
+    assert np.array_equal(bits(acc), bits(fixture["accum_96x54_spp16_s0"]))
+    assert np.array_equal(rgba, fixture["rgba_96x54_spp16_s0"])
+    c.close()

@@ -20,16 +20,22 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--sections", action="store_true", help="print the wave-cycle split of an RT_SECTIONS build")
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    ap.add_argument("--reps", type=int, default=1, help="measured renders after the warm-up")
     args = ap.parse_args()
     spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(PKG, "__init__.py"))
     rt = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(rt)
     rt.LIB_PATH = os.path.join(PKG, args.lib)
     c = rt.Context(0)
-    c.upload(rt.Scene.cornell())
+    if args.scene == "c5":
+        import numpy as np
+        c.upload(rt.Scene.cornell_c5(np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"]))
+    else:
+        c.upload(rt.Scene.cornell())
     c.resize(args.width, args.height)
     cam, _, _ = rt.camera_default(args.width, args.height)
-    for _ in range(2):
+    for _ in range(1 + args.reps):
         c.render(cam, args.spp, fetch=False, exact=not args.fast)
     st = c.stats()
     print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
