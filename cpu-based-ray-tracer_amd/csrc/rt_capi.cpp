@@ -549,6 +549,14 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.W = c->W; P.H = c->H;
     P.first_frame = p->first_frame; P.n_frames = p->n_frames;
     P.seed = p->seed; P.rr = p->rr;
+    {   // IEEE single divisions on the host: exactly the kernels' constants and correctly rounded reciprocals
+        const float pdf = 1.0f / (2.0f * 3.141592653589793f);
+        P.y_pdf = 1.0f / pdf;
+        P.y_rr = p->rr > 0.0f ? 1.0f / p->rr : 0.0f;
+        P.lpdf = 1.0f / c->hdr.light_area;
+        P.y_lpdf = 1.0f / P.lpdf;
+        P.y_w = 1.0f / (float)c->W; P.y_h = 1.0f / (float)c->H;
+    }
     P.band = c->band; P.rank = c->rank; P.nranks = c->nranks; P.n_local_rows = c->local_rows;
     P.tiles_x = (c->W + 7) / 8;
     const uint64_t items = (uint64_t)((c->local_rows + 7) / 8) * P.tiles_x * 64;

@@ -285,6 +285,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint16_t* const plist = reinterpret_cast<uint16_t*>(lstate + (P.has_light ? (EXACT ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256u) +
                             (threadIdx.x >> 6) * P.pair_cap;
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
+    // the leaf-box variant divides with rt_device.h div_fast (y = the divisor's correctly rounded
+    // reciprocal; C4 +1.1 %); the BVH variant keeps the IEEE division sequence (its register budget: C5
+    // -2 % with div_fast)
+    auto sdiv = [](float x, float d, float y) { return BVH ? x / d : div_fast(x, d, y); };
+    auto vdiv = [](V3 a, float d, float y) { return BVH ? divs(a, d) : divs_fast(a, d, y); };
     // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
     // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
     // pixel's samples in frame order (MC/Renderer.cpp:128-133).  The kernel issues no global load
@@ -322,7 +327,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 if (j < dleft) {
                     const float4 mb2 = S.mats[2 * m[j]];
                     const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                    L = add(V3{e[j].x, e[j].y, e[j].z}, divs(divs(muls(mul(L, f), e[j].w), PDF), Q.rr));
+                    L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
                 }
             }
             const uint32_t n = dleft < RT_DRAIN_STEP ? dleft : RT_DRAIN_STEP;
@@ -342,7 +347,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         ring_load(Q, RING_AT(pos), e, m);
         const float4 mb2 = S.mats[2 * m];
         const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-        const V3 L = add(V3{e.x, e.y, e.z}, divs(divs(muls(mul(ls3(VS_DL), f), e.w), PDF), Q.rr));
+        const V3 L = add(V3{e.x, e.y, e.z}, vdiv(vdiv(muls(mul(ls3(VS_DL), f), e.w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
         dleft = dleft - 1u;
         if (dleft == 0u) {
             complete(L, lsu(VS_DT0), lsu(VS_DT1));
@@ -375,7 +380,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 if (j < dleft) {
                     const float4 mb2 = S.mats[2 * m[j]];
                     const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                    L = add(V3{e[j].x, e[j].y, e[j].z}, divs(divs(muls(mul(L, f), e[j].w), PDF), Q.rr));
+                    L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
                 }
             }
             const uint32_t n = dleft < RT_DRAIN_BATCH ? dleft : RT_DRAIN_BATCH;
@@ -570,7 +575,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const float c = lsf(VS_PCOS);
                         const float4 mb = S.mats[2 * lsu(VS_MAT)];
                         const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        st3(VS_THR, muls(mul(thr, f), c / PDF / Q.rr));
+                        st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
                         if (triA < 0 || emissive) { L = lsum; finished = true; }
                         else vertex = true;
                     }
@@ -655,8 +660,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
                         const float4 mb = S.mats[2 * mat];
                         const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        st3(VS_LD, divs(divs(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2),
-                                        (1.0f / Q.light_area)));
+                        st3(VS_LD, vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
+                                             BVH ? 0.0f : rcp_f32(sd2)),
+                                        Q.lpdf, Q.y_lpdf));   // Q.lpdf = 1.0f / light_area
                         dB = wl;
                         hasB = true;
                     }
@@ -755,13 +761,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #if RT_SECTIONS
             dbg_cam = true;
 #endif
-            float cx = ((float)x + ux) / (float)Q.W;
-            float cy = ((float)y + uy) / (float)Q.H;
+            float cx = sdiv((float)x + ux, (float)Q.W, Q.y_w);
+            float cy = sdiv((float)y + uy, (float)Q.H, Q.y_h);
             cx = cx * 2.0f - 1.0f;
             cy = cy * 2.0f - 1.0f;
             float tg[4];
             mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(divs(V3{tg[0], tg[1], tg[2]}, tg[3]));
+            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
             float wd[4];
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};

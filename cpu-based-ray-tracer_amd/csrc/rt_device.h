@@ -52,6 +52,25 @@ __device__ __forceinline__ float rcp_f32(float x)
     return 1.0f / x;
 }
 
+// x / d correctly rounded, from y = RN(1/d): q = RN(x * y), the exact residual r = x - q * d (one fma),
+// then RN(q + r * y) -- Markstein's correction.  Checked bit for bit against the IEEE division for every
+// x with 2^-100 <= |x| < 2^100 and a list of divisors (tools/verify_div.hip); div_fast takes the IEEE
+// division outside that range and for divisors outside [2^-20, 2^20).
+__device__ __forceinline__ float div_fast_core(float x, float d, float y)
+{
+    const float q = x * y;
+    const float r = __builtin_fmaf(-q, d, x);
+    return __builtin_fmaf(r, y, q);
+}
+__device__ __forceinline__ float div_fast(float x, float d, float y)
+{
+    const float ax = __builtin_fabsf(x), ad = __builtin_fabsf(d);
+    if (ax >= 0x1p-100f && ax < 0x1p100f && ad >= 0x1p-20f && ad < 0x1p20f) return div_fast_core(x, d, y);
+    return x / d;
+}
+
+__device__ __forceinline__ V3 divs_fast(V3 a, float d, float y) { return V3{div_fast(a.x, d, y), div_fast(a.y, d, y), div_fast(a.z, d, y)}; }
+
 // glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
 __device__ __forceinline__ V3 glm_normalize(V3 v) { float is = rcp_f32(__builtin_sqrtf(dot(v, v))); return muls(v, is); }
 __device__ __forceinline__ float glm_length(V3 v) { return __builtin_sqrtf(dot(v, v)); }
@@ -78,12 +97,13 @@ constexpr float INTERSECTION_CORRECTION = 0.00001f;   // MC/WhittedUtilities.h:1
 // (Walnut::Random::Float, WN/Random.h:27-30).
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4])
 {
+    // each 32 x 32 -> 64-bit product as ONE v_mad_u64_u32 (the split __umulhi + low multiply is two
+    // quarter-rate instructions)
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
@@ -176,15 +196,16 @@ __device__ __forceinline__ bool moller_trumbore_od(const V3& a, const V3& e1, co
     const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
     const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
     if (!(pos || ngt)) return false;
-    if ((__builtin_fabsf(b2n) + __builtin_fabsf(b3n)) > __builtin_fabsf(den) * 1.00001f) return false;
+    const float sb = __builtin_fabsf(b2n) + __builtin_fabsf(b3n), aden = __builtin_fabsf(den);
+    if (sb > aden * 1.00001f) return false;
     const double inv = rcp_f64_of_f32(den);   // == 1.0 / (double)den
     const double t = (double)tn * inv;
-    const double b2 = (double)b2n * inv;
-    const double b3 = (double)b3n * inv;
     t_out = t;
     // b2 > 0 and b3 > 0 follow from t > 0: tn, b2n, b3n share one strict sign (above), inv is finite
     // and nonzero or NaN (den = +-inf: NaN, t > 0 fails as the reference's t = +-0 does), and no product
     // of a nonzero float with inv underflows or overflows in double
+    const double b2 = (double)b2n * inv;
+    const double b3 = (double)b3n * inv;
     return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
 }
 __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
