@@ -312,6 +312,29 @@ __device__ __forceinline__ float sin_f(float y)
     return (float)r;
 }
 
+// cos_f(y) and sin_f(y) together, branch-free: one reduction, each polynomial once (cos_f and sin_f
+// evaluate the same two polynomials of the same reduced argument and pick / negate by the quadrant).
+__device__ __forceinline__ void sincos_f(float y, float& c, float& s)
+{
+    using namespace glibc_trig;
+    const double x = y;
+    const bool small = top12(y) < top12(0x1.921FB6p-1f);   // |y| < pi/4: no reduction, n = 0
+    int nr;
+    const double xr0 = reduce(x, nr);
+    const int n = small ? 0 : nr;
+    const double xr = small ? x : xr0;
+    const double sg = (n & 2) ? ((n & 1) ? 1.0 : -1.0) : ((n & 1) ? -1.0 : 1.0);   // sign[n & 3]
+    const double x2 = xr * xr;
+    const double ps = poly(xr * sg, x2, 0), pc = poly(xr * sg, x2, 1);
+    const double npc = (n & 2) ? -pc : pc;
+    double rc = (n & 1) ? ps : npc;
+    double rs = (n & 1) ? npc : ps;
+    float fc = (float)rc, fs = (float)rs;
+    if (top12(y) < top12(0x1p-12f)) { fc = 1.0f; fs = y; }   // the tiny-argument returns
+    c = fc;
+    s = fs;
+}
+
 // powf of the specular lobe (WH/Renderer.h:287-292: std::powf -> glibc powf).  Evaluated as
 // exp(y * log(x)) in double and rounded once to float: correctly rounded except within ~1e-15 of a
 // rounding boundary, as glibc's powf (double-precision log2/exp2 core) is; x >= 0 here.

@@ -684,8 +684,10 @@ __global__ void math_kernel(uint32_t n, const float* __restrict__ x, float* __re
     const float v = x[i];
     out[7 * i + 0] = __builtin_sqrtf(v);
     out[7 * i + 1] = rcp_f32(v);   // the kernels' reciprocal (rt_device.h); == 1.0f / v correctly rounded
-    out[7 * i + 2] = cos_f(v);
-    out[7 * i + 3] = sin_f(v);
+    float cv, sv;
+    sincos_f(v, cv, sv);   // what sample_hemisphere evaluates (rt_path.h)
+    out[7 * i + 2] = cv;
+    out[7 * i + 3] = sv;
     const double r = rcp_f64_of_f32(v);   // Moller-Trumbore's 1 / (double)den (rt_device.h)
     out[7 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
     out[7 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));

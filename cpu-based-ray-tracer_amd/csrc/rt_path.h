@@ -146,8 +146,10 @@ __device__ __forceinline__ V3 sample_hemisphere(V3 n, G& g)
     const float z = g.next();
     const float rxy = __builtin_sqrtf(1.0f - z * z);
     const float phi = 2.0f * PI_F * g.next();
-    const float x = rxy * cos_f(phi);
-    const float y = rxy * sin_f(phi);
+    float cphi, sphi;
+    sincos_f(phi, cphi, sphi);
+    const float x = rxy * cphi;
+    const float y = rxy * sphi;
     V3 Y;
     if (__builtin_fabsf(n.x) > __builtin_fabsf(n.y)) Y = glm_normalize(V3{n.z, 0.0f, -(n.x)});
     else Y = glm_normalize(V3{0.0f, n.z, -(n.y)});
