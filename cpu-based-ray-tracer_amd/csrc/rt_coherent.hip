@@ -169,8 +169,8 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_REP_MT
 #define RT_REP_MT 1
 #endif
-// section timing (diagnostic builds): wave cycles spent in service-head / vertex / finish / queue /
-// camera / box loop / Moller-Trumbore, summed into counters[16..23]
+// section timing (diagnostic builds): wave cycles spent in fold drain (top) / vertex / finish / work queue +
+// service head / camera / box loop / Moller-Trumbore, summed into counters[16..23]
 #ifndef RT_SECTIONS
 #define RT_SECTIONS 0
 #endif
@@ -494,6 +494,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
             }
         }
+        SEC_MARK(3);
         // ======================= lane-level work queue (wave-collective) =======================
         // at the top of the iteration, before any store: a lane that finished its item in the previous
         // iteration takes the next one (the returning atomic waits for no store of this iteration).
@@ -750,7 +751,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
         }
 
-        SEC_MARK(3);
         SEC_MARK(4);
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
@@ -876,7 +876,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             SEC_SUM(13, (uint32_t)__popcll(ca));
             const uint32_t tot = sec_w[15];
             SEC_COUNT(8, (tot + 63u) >> 6);
-            // the wave's distinct candidate triangles: ray A's, ray B's, either
+#if RT_SECTIONS >= 2
+            // the wave's distinct candidate triangles: ray A's, ray B's, either (its own build: the loop
+            // is timed with the Moller-Trumbore section)
             uint32_t ua = 0, ub = 0, uab = 0;
             for (uint32_t t = 0; t < 64u; ++t) {
                 const bool a_ = __ballot(((ca >> t) & 1u) != 0u) != 0, b_ = __ballot(((cb >> t) & 1u) != 0u) != 0;
@@ -885,6 +887,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             SEC_COUNT(16, ua);
             SEC_COUNT(17, ub);
             SEC_COUNT(18, uab);
+#endif
         }
 #endif
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins

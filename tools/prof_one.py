@@ -41,7 +41,7 @@ def main():
     print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
     if args.sections:
         cyc = c.debug_counters(24)[16:24]
-        names = ["service head", "vertex", "finish", "queue", "camera", "box loop", "moller-trumbore", "(entry)"]
+        names = ["fold drain (top)", "vertex", "finish", "queue + service head", "camera", "box loop", "moller-trumbore", "(entry)"]
         tot = float(sum(cyc)) or 1.0
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
         n = c.debug_counters(44)[24:44]
