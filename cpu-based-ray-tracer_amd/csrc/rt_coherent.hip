@@ -115,6 +115,10 @@ struct VertexRng {
 // the three sign bits of the direct term (one 16-byte load instead of two)
 __device__ __forceinline__ void ring_load(const CKParams& Q, size_t at, float4& e, int& m)
 {
+#if RT_DIAG_NO_RING_LOAD
+    // cost attribution only (wrong images): the ring loads replaced by a value derived from the address
+    e = make_float4(0.1f, 0.1f, 0.1f, (float)(at & 7u) * 0.1f); m = 1; return;
+#endif
     e = Q.stack_ld[at];
     if (Q.ring_pack) {
         const uint32_t x = __float_as_uint(e.x), y = __float_as_uint(e.y), z = __float_as_uint(e.z);
