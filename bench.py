@@ -287,7 +287,9 @@ def main():
         roof["counters"] = {"file": pmc["_file"], "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
                             "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                             "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample"),
-                            "kernel_ms_profiled": pmc.get("kernel_ms")}
+                            "kernel_ms_profiled": pmc.get("kernel_ms"), "traffic_method": pmc.get("hbm_correction"),
+                            "read_bytes_per_sample": pmc.get("split_read_bytes_per_sample"),
+                            "write_bytes_per_sample": pmc.get("split_write_bytes_per_sample")}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -31,7 +31,10 @@ struct rt_ctx {
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
     bool qbvh = false;                             // RT_QBVH=1: the BVH variant walks the compact BVH (A/B: slower)
-    bool ring_pack = true;                         // RT_RING_PACK=0: fold-level materials in their own array
+    // fold-level materials in the direct term's sign bits (one 16-byte ring entry per level instead of an
+    // entry plus a 4-byte material that misses L2 on its own line: C4 221 -> 133 B/sample of L2 -> fabric
+    // traffic): RT_RING_PACK 0 off, 1 BVH variant only, 2 both variants
+    uint32_t ring_pack = 2;
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
@@ -77,7 +80,8 @@ struct rt_ctx {
     // per lane, into about items_per_lane items per lane but no chunk shorter than min_chunk_frames
     // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
     uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 16;
-    uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch (RT_LBUF_BUDGET_MB); C4 needs 20 GB of 288
+    uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch; C4 needs 25 GB of 288
+    bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(32 GB, 3/4 of free memory) per render
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
@@ -378,13 +382,16 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_PAIR_CAP")) c->pair_cap_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_RING_PACK")) c->ring_pack = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_MIN_CHUNK_FRAMES")) c->min_chunk_frames = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
-    if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+    if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) {
+        c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
+        c->lbuf_budget_env = true;
+    }
     if (const char* e = std::getenv("RT_STACK_DEPTH")) c->stack_depth_force = std::min<uint32_t>(kStackDepthMax, (uint32_t)std::strtoul(e, nullptr, 10));
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
@@ -596,9 +603,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     }
     if (coh_bvh) {   // the BVH variant reads the scene from HBM
         P.lds_scene_quads = 0;
-        P.ring_pack = (c->ring_pack && c->hdr.n_mats <= 8) ? 1u : 0u;
+        P.ring_pack = (c->ring_pack >= 1 && c->hdr.n_mats <= 8) ? 1u : 0u;
         P.thresh = c->vthresh; P.steps = c->vsteps;
     }
+    if (coh_box && exact) P.ring_pack = (c->ring_pack >= 2 && c->hdr.n_mats <= 8) ? 1u : 0u;
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy
     // (4 workgroups of 256 lanes per CU = 40 KiB each), at most 8
     P.lds_levels = 0;
@@ -662,6 +670,13 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             // frames of chunks >= 1
             const bool park_all = coh;
             uint32_t passes = 1;
+            if (!c->lbuf_budget_env) {
+                // parked-sample budget from the device's free memory (the current buffer counts as free):
+                // at most 32 GB, at most 3/4 of what is free
+                size_t fr = 0, tot = 0;
+                HIPC(c, hipMemGetInfo(&fr, &tot));
+                c->lbuf_budget = std::max<uint64_t>(64ull << 20, std::min<uint64_t>(32ull << 30, (fr + c->lbuf_floats * sizeof(float)) / 4 * 3));
+            }
             if (want > 1 || park_all) {
                 const uint64_t bytes = px_local * (uint64_t)p->n_frames * 12ull;
                 passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
@@ -678,7 +693,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 Q.n_chunks = n_chunks; Q.chunk_frames = F; Q.items_per_chunk = (uint32_t)items_px;
                 Q.park_all = park_all ? 1u : 0u;
                 Q.lbuf_pixel_major = park_all && c->lbuf_pm ? 1u : 0u;
-                if (items_px * n_chunks >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
+                // the 32-bit work counter runs past n_items by the last refills (each wave takes 64 items
+                // per atomic until it sees the queue empty, a few refills at most): keep 4 per wave of headroom
+                if (items_px * n_chunks + lanes * 4ull >= 0xFFFFFFFFull) { c->err = "too many work items for one launch"; return RT_ERR_INVALID; }
                 Q.n_items = (uint32_t)(items_px * n_chunks);
                 if (n_chunks > 1 || park_all) {
                     // 4-frame blocks of 12 floats per pixel (rt_kernels.hip)

@@ -162,6 +162,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #endif
 // work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
 // more than one item per lane, so the launch tail stays one item long)
+#ifndef RT_PARK_NT
+#define RT_PARK_NT 0   // 1: parked samples with non-temporal stores (A/B)
+#endif
 #ifndef WQ_BATCH
 #define WQ_BATCH 64u
 #endif
@@ -305,9 +308,16 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         const size_t blk = Q.lbuf_pixel_major ? (size_t)local * ((Q.n_frames + 3u) >> 2) + (fidx >> 2)
                                               : (size_t)(fidx >> 2) * Q.lbuf_stride + local;
         const size_t at = (blk * 4u + (fidx & 3u)) * 3u;
+#if RT_PARK_NT
+        // write-once data: streaming stores, so parked lines do not evict the fold ring's lines from L2
+        __builtin_nontemporal_store(L.x, &Q.lbuf[at]);
+        __builtin_nontemporal_store(L.y, &Q.lbuf[at + 1]);
+        __builtin_nontemporal_store(L.z, &Q.lbuf[at + 2]);
+#else
         Q.lbuf[at] = L.x;
         Q.lbuf[at + 1] = L.y;
         Q.lbuf[at + 2] = L.z;
+#endif
     };
     // one fold step of the draining path: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
     // (MC/Renderer.cpp:208,213), inner level first

@@ -262,11 +262,12 @@ def test_vertex_kernel_equals_megakernel(monkeypatch, exact):
     """Small scenes render with the vertex-synchronous kernel (rt_coherent.hip); RT_VERTEX=0 runs the
     general megakernel, RT_FORCE_WALK=1 sends every ray of the vertex kernel through its per-lane BVH
     walk (the path of rays with a non-finite reciprocal direction).  Same bits in EXACT and FAST mode,
-    with and without frame chunks."""
+    with and without frame chunks, with the fold levels' materials in the direct term's sign bits (the
+    default) or in their own array (RT_RING_PACK=0)."""
     out = {}
     for name, env in (("vertex", {}), ("mega", {"RT_VERTEX": "0"}), ("walk", {"RT_FORCE_WALK": "1"}),
-                      ("vertex_chunks", {"RT_CHUNKS": "3"})):
-        for k in ("RT_VERTEX", "RT_FORCE_WALK", "RT_CHUNKS"):
+                      ("vertex_chunks", {"RT_CHUNKS": "3"}), ("ring_mat_array", {"RT_RING_PACK": "0"})):
+        for k in ("RT_VERTEX", "RT_FORCE_WALK", "RT_CHUNKS", "RT_RING_PACK"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -279,7 +280,7 @@ def test_vertex_kernel_equals_megakernel(monkeypatch, exact):
             out[name] = (rgba, a)
         finally:
             c.close()
-    for name in ("mega", "walk", "vertex_chunks"):
+    for name in ("mega", "walk", "vertex_chunks", "ring_mat_array"):
         assert np.array_equal(out[name][0], out["vertex"][0]), name
         assert np.array_equal(bits(out[name][1]), bits(out["vertex"][1])), name
 
