@@ -123,7 +123,8 @@ __device__ __forceinline__ void ring_load(const CKParams& Q, size_t at, float4& 
     if (Q.ring_pack) {
         const uint32_t x = __float_as_uint(e.x), y = __float_as_uint(e.y), z = __float_as_uint(e.z);
         m = (int)((x >> 31) | ((y >> 30) & 2u) | ((z >> 29) & 4u));
-        e = make_float4(__uint_as_float(x & 0x7FFFFFFFu), __uint_as_float(y & 0x7FFFFFFFu), __uint_as_float(z & 0x7FFFFFFFu), e.w);
+        // |x| as fabsf: the fold's adds take it as a free source modifier
+        e = make_float4(__builtin_fabsf(e.x), __builtin_fabsf(e.y), __builtin_fabsf(e.z), e.w);
     } else {
         m = Q.stack_mat[at];
     }

@@ -59,7 +59,9 @@ def main():
     lines = []
     # C1: the Whitted world, 640x480, 50 frames (identical: deterministic)
     dt = timed([os.path.join(REF, "ref_whitted_spheres"), "image", "640", "480", "50", T] + out)
-    lines.append({"config": "C1", "samples": 640 * 480 * 50, "seconds": dt, "note": "50 frames"})
+    # (the harness traces each pixel once and accumulates that color 50 times -- the frames are identical --
+    # so one frame's pixels are the traced samples)
+    lines.append({"config": "C1", "samples": 640 * 480, "seconds": dt, "note": "one traced frame (50 identical frames accumulated)"})
     # C2 / C4: Cornell MC at reduced spp (frames are i.i.d., time is linear in spp), shipped RNG
     def bench_mt(extra, W, H, spp):
         r = subprocess.run([os.path.join(REF, "ref_harness"), "bench_mt", tmp, extra, str(W), str(H), str(spp), "0.8", T],

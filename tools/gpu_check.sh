@@ -18,3 +18,7 @@ tail -1 "$OUT/bench.log"
 if [ "${PROFILE:-1}" = "1" ]; then
   bash profiles/run_rocprof.sh "$TAG"
 fi
+if [ "${SECTIONS:-0}" = "1" ] && [ -f cpu-based-ray-tracer_amd/librt_hip_sec.so ]; then
+  timeout -k 10 200 python3 tools/prof_one.py librt_hip_sec.so --sections --spp 256 > "$OUT/sections_c4_256spp.txt" 2>&1
+  timeout -k 10 200 python3 tools/prof_one.py librt_hip_sec.so --sections --scene c5 --spp 16 > "$OUT/sections_c5_16spp.txt" 2>&1
+fi
