@@ -35,6 +35,7 @@ struct rt_ctx {
     // entry plus a 4-byte material that misses L2 on its own line: C4 221 -> 133 B/sample of L2 -> fabric
     // traffic): RT_RING_PACK 0 off, 1 BVH variant only, 2 both variants
     uint32_t ring_pack = 2;
+    bool bvh_small_lds = true;   // RT_BVH_SMALL_LDS=0: the BVH variant reads materials and light tables from HBM
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
@@ -383,6 +384,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_PAIR_CAP")) c->pair_cap_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -592,7 +594,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
     // any other path scene: its BVH variant, the scene in HBM (RT_VERTEX_BVH=0: the megakernel)
     const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
-    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted;
+    // (the BVH variant keeps the hit triangle's material beside its index: < 2^24 triangles, < 128 materials)
+    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 24) &&
+                         P.n_mats < 128u;
     const bool coh = coh_box || coh_bvh;
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
@@ -601,8 +605,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
         P.lds_scene_quads -= 2 * P.n_lboxes + 2 * P.n_nodes;
     }
-    if (coh_bvh) {   // the BVH variant reads the scene from HBM
-        P.lds_scene_quads = 0;
+    if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; materials and the light
+        // tables stay in LDS when they are small (C5: 21 quads)
+        const uint32_t small = 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris;
+        P.lds_scene_quads = (c->bvh_small_lds && small <= 64u) ? small : 0u;
         P.ring_pack = (c->ring_pack >= 1 && c->hdr.n_mats <= 8) ? 1u : 0u;
         P.thresh = c->vthresh; P.steps = c->vsteps;
     }
@@ -617,7 +623,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             if (occupancy(used + rt_stack_lds_bytes(lv)) >= occ0) { P.lds_levels = lv; break; }
     }
     if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
-    size_t shmem = (lds && !coh_bvh ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
+    size_t shmem = ((lds || coh_bvh) ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
     P.pair_cap = 0;
     if (coh_box) {

@@ -163,6 +163,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #endif
 // work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
 // more than one item per lane, so the launch tail stays one item long)
+#ifndef RT_HIT_MAT
+#define RT_HIT_MAT 0   // 1: BVH variant keeps the hit triangle's material beside its index (C5 -1.5 %: spills)
+#endif
 #ifndef RT_PARK_NT
 #define RT_PARK_NT 0   // 1: parked samples with non-temporal stores (A/B)
 #endif
@@ -262,6 +265,19 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     S.n_nodes = P.n_nodes;
     if (BVH) {
         S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = nullptr;
+        if (P.lds_scene_quads != 0u) {
+            // the small tables in LDS (mats | lnodes | ltris): the service's material and the light
+            // sample then wait on no HBM load
+            const uint32_t mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
+            float4* dm = lds_scene;
+            float4* dl = dm + mq;
+            float4* dlt = dl + lq;
+            for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
+            for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
+            for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
+            __syncthreads();
+            S.mats = dm; S.lnodes = dl; S.ltris = dlt;
+        }
     } else {
         // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris; the leaf boxes
         // are read with scalar loads)
@@ -572,7 +588,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             int mat = 0;
             bool emissive = false;
             if (hasA && triA >= 0) {
-                mat = (BVH && kargs4().use_qnodes) ? f2i(kargs4().tabc[3 * triA].w) : f2i(S.tris[4 * triA].w);
+                // BVH variant: the material came with the hit (tri_mat)
+                mat = (BVH && RT_HIT_MAT) ? (triA >> 24) : f2i(S.tris[4 * (BVH ? (triA & 0xFFFFFF) : triA)].w);
                 emissive = S.mats[2 * mat].w != 0.0f;
             }
             bool vertex = false;
@@ -657,7 +674,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
-                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[triA] : S.tris[4 * triA + 3];
+                const int ti3 = BVH ? (triA & 0xFFFFFF) : triA;
+                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[4 * ti3 + 3];
                 const V3 wo = neg(dA);
                 const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
                 const V3 N{tq3.x, tq3.y, tq3.z};
@@ -1124,9 +1142,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const int pk = slot == 0 ? parked0 : parked1;
                         if (pk < 0 || (!curA && occB)) continue;
                         V3 va, e1, e2;
+                        int pmat;   // the triangle's material, kept with the hit (the service reads no triangle)
                         if (qround) {
                             const float4* ta = kargs4().tabc + 3 * pk;
                             const float4 t0 = ta[0], t1 = ta[1], t2 = ta[2];
+                            pmat = f2i(t0.w);
                             // the exact leaf box: Triangle::Get3DAABB (MC/TriangleMesh.h:96-99)
                             if (!slab_hit_finite(r, __builtin_fminf(__builtin_fminf(t0.x, t1.x), t2.x), __builtin_fminf(__builtin_fminf(t0.y, t1.y), t2.y),
                                                  __builtin_fminf(__builtin_fminf(t0.z, t1.z), t2.z), __builtin_fmaxf(__builtin_fmaxf(t0.x, t1.x), t2.x),
@@ -1138,11 +1158,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         } else {
                             const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
                             va = V3{t0.x, t0.y, t0.z}; e1 = V3{t1.x, t1.y, t1.z}; e2 = V3{t2.x, t2.y, t2.z};
+                            pmat = f2i(t0.w);
                         }
                         double t;
                         if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {
-                                if (t <= tA) { tA = t; triA = pk; }   // the later leaf wins ties
+                                // the later leaf wins ties; the index in bits 0-23, the material above
+                                if (t <= tA) { tA = t; triA = pk | (RT_HIT_MAT ? (pmat << 24) : 0); }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 ti = NN;

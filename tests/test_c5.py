@@ -127,11 +127,13 @@ def test_full_frame_digest(ctx, fixture):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"}])
+@pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"},
+                                 {"RT_BVH_SMALL_LDS": "0"}])
 def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):
     """The vertex kernel's BVH variant (the C5 path) on the reference's 96x54x16 accumulation, with the
-    fold-level materials in their own array or in the direct term's sign bits, and walking the exact
-    nodes or the compact BVH (16-bit outward-rounded boxes, exact leaf boxes from the vertices)"""
+    fold-level materials in their own array or in the direct term's sign bits, walking the exact
+    nodes or the compact BVH (16-bit outward-rounded boxes, exact leaf boxes from the vertices), and
+    with the materials and light tables in LDS (default) or read from HBM"""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     c = rt.Context(0)
