@@ -601,7 +601,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };
-    const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0) : rt_lane_state_lds_bytes(exact);
+    const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0, coh_bvh) : rt_lane_state_lds_bytes(exact);
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
         P.lds_scene_quads -= 2 * P.n_lboxes + 2 * P.n_nodes;
     }

@@ -50,7 +50,9 @@ enum : uint32_t {
     VS_THR = 8, VS_LSUM = 11,            // FAST: throughput, radiance
     VS_WORDS_EXACT = 15, VS_WORDS_FAST = 14,
     VS_RNG = 15,                         // unlit scenes only: the Philox block of the current 4 draws
-    VS_WORDS_UNLIT = 19
+    VS_WORDS_UNLIT = 19,
+    // BVH variant (RT_HIT_MAT 2): the closest hit's material, one word after the scene's lane state
+    VS_HMAT_LIT = 15, VS_HMAT_UNLIT = 19
 };
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
@@ -164,7 +166,7 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
 // more than one item per lane, so the launch tail stays one item long)
 #ifndef RT_HIT_MAT
-#define RT_HIT_MAT 0   // 1: BVH variant keeps the hit triangle's material beside its index (C5 -1.5 %: spills)
+#define RT_HIT_MAT 0   // BVH variant, the closest hit's material kept 1: beside its index, 2: in an LDS word (C5 -1.5 % / -2.4 %: spills)
 #endif
 #ifndef RT_PARK_NT
 #define RT_PARK_NT 0   // 1: parked samples with non-temporal stores (A/B)
@@ -589,7 +591,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             bool emissive = false;
             if (hasA && triA >= 0) {
                 // BVH variant: the material came with the hit (tri_mat)
-                mat = (BVH && RT_HIT_MAT) ? (triA >> 24) : f2i(S.tris[4 * (BVH ? (triA & 0xFFFFFF) : triA)].w);
+                mat = (BVH && RT_HIT_MAT == 1) ? (triA >> 24)
+                    : (BVH && RT_HIT_MAT == 2) ? (int)lsu(P.has_light ? VS_HMAT_LIT : VS_HMAT_UNLIT)
+                                               : f2i(S.tris[4 * (BVH ? (triA & 0xFFFFFF) : triA)].w);
                 emissive = S.mats[2 * mat].w != 0.0f;
             }
             bool vertex = false;
@@ -674,7 +678,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
-                const int ti3 = BVH ? (triA & 0xFFFFFF) : triA;
+                const int ti3 = (BVH && RT_HIT_MAT == 1) ? (triA & 0xFFFFFF) : triA;
                 const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[4 * ti3 + 3];
                 const V3 wo = neg(dA);
                 const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
@@ -1164,7 +1168,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {
                                 // the later leaf wins ties; the index in bits 0-23, the material above
-                                if (t <= tA) { tA = t; triA = pk | (RT_HIT_MAT ? (pmat << 24) : 0); }
+                                if (t <= tA) {
+                                    tA = t;
+                                    triA = pk | (RT_HIT_MAT == 1 ? (pmat << 24) : 0);
+                                    if (RT_HIT_MAT == 2) lsu(kargs4().has_light ? VS_HMAT_LIT : VS_HMAT_UNLIT) = (uint32_t)pmat;
+                                }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 ti = NN;
@@ -1237,8 +1245,9 @@ hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* m
     return hipGetLastError();
 }
 
-size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit)
+size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh)
 {
+    if (bvh && RT_HIT_MAT == 2) return (size_t)((lit ? VS_HMAT_LIT : VS_HMAT_UNLIT) + 1) * 256 * sizeof(float);
     return (size_t)(lit ? (exact ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
 }
 

@@ -81,7 +81,7 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
 // scene in LDS: LDS = scene | lane state) or, bvh = true, any scene in HBM (LDS = lane state)
 hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
 int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes);
-size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit);
+size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);
 // Whitted Style Ray Tracer world (spheres + textured meshes, reflection/refraction recursion), config C1
