@@ -165,6 +165,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #endif
 // work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
 // more than one item per lane, so the launch tail stays one item long)
+#ifndef RT_LATE_ITEMS
+#define RT_LATE_ITEMS 1   // a lane whose item ended takes the next from the wave's pool in the same iteration (C4 +0.4 %, C5 +1.4 %)
+#endif
 #ifndef RT_HIT_MAT
 #define RT_HIT_MAT 0   // BVH variant, the closest hit's material kept 1: beside its index, 2: in an LDS word (C5 -1.5 % / -2.4 %: spills)
 #endif
@@ -490,6 +493,57 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #define SEC_SUM(i, v) do { } while (0)
 #define SEC_MARK(k) do { } while (0)
 #endif
+    // Lanes without a work item take the next ones from the wave's pool, in lane order.  With `refill`
+    // (the top of the iteration, before any store) an empty pool is refilled from the device counter;
+    // without it (RT_LATE_ITEMS: after the path-end block, so a lane whose item just ended starts the
+    // next one's camera ray in the same iteration) only the pool's items are handed out -- no atomic,
+    // so nothing waits for the iteration's stores.
+    auto take_items = [&](const bool refill) {
+        const bool need = alive && !have_pixel;
+        const uint64_t mask = __ballot(need);
+        if (mask == 0) return;
+        CKParams& Q = kargs4();
+        uint32_t n = (uint32_t)__popcll(mask);
+        if (!refill && n > pool_count) n = pool_count;
+        if (n == 0) return;
+        uint32_t fresh = 0;   // first item of a new batch (wave-uniform)
+        if (n > pool_count) {
+            uint32_t b = 0;
+            if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, WQ_BATCH);
+            fresh = __builtin_amdgcn_readfirstlane(b);
+        }
+        const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (need && j < n) {
+            const uint32_t w = j < pool_count ? pool_base + j : fresh + (j - pool_count);
+            if (w >= Q.n_items) {
+                alive = false;
+            } else {
+                // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
+                const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
+                const uint32_t tile = wp >> 6, within = wp & 63u;
+                const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
+                const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
+                if (lr < Q.n_local_rows && lx < Q.W) {
+                    // local row -> global row (row bands dealt round-robin over ranks)
+                    const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+                    const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
+                    const uint32_t local = lr * Q.W + lx;
+                    lsu(VS_LOCAL) = local;
+                    lsu(VS_PIX) = y * Q.W + lx;
+                    lsu(VS_FRAME) = Q.first_frame + c * Q.chunk_frames;   // the frame of the item's first sample
+                    have_pixel = true;
+                    k = 0;
+                }
+            }
+        }
+        if (n > pool_count) {
+            pool_base = fresh + (n - pool_count);
+            pool_count = WQ_BATCH - (n - pool_count);
+        } else {
+            pool_base += n;
+            pool_count -= n;
+        }
+    };
     for (;;) {
         SEC_MARK(0);
 #if RT_PAD_VALU
@@ -535,49 +589,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // (two uniform registers); lanes are served from the pool in lane order.  One returning atomic
         // on one word saturates near 88 dequeues/us (MI355X_MICROARCH.md, dequeue): one per refill
         // (a lane or two per wave and iteration) was the limit at 16-frame chunks.
-        const bool need = alive && !have_pixel;
-        const uint64_t mask = __ballot(need);
-        if (mask != 0) {
-            CKParams& Q = kargs4();
-            const uint32_t n = (uint32_t)__popcll(mask);
-            uint32_t fresh = 0;   // first item of a new batch (wave-uniform)
-            if (n > pool_count) {
-                uint32_t b = 0;
-                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, WQ_BATCH);
-                fresh = __builtin_amdgcn_readfirstlane(b);
-            }
-            if (need) {
-                const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                const uint32_t w = j < pool_count ? pool_base + j : fresh + (j - pool_count);
-                if (w >= Q.n_items) {
-                    alive = false;
-                } else {
-                    // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
-                    const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
-                    const uint32_t tile = wp >> 6, within = wp & 63u;
-                    const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
-                    const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
-                    if (lr < Q.n_local_rows && lx < Q.W) {
-                        // local row -> global row (row bands dealt round-robin over ranks)
-                        const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
-                        const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
-                        const uint32_t local = lr * Q.W + lx;
-                        lsu(VS_LOCAL) = local;
-                        lsu(VS_PIX) = y * Q.W + lx;
-                        lsu(VS_FRAME) = Q.first_frame + c * Q.chunk_frames;   // the frame of the item's first sample
-                        have_pixel = true;
-                        k = 0;
-                    }
-                }
-            }
-            if (n > pool_count) {
-                pool_base = fresh + (n - pool_count);
-                pool_count = WQ_BATCH - (n - pool_count);
-            } else {
-                pool_base += n;
-                pool_count -= n;
-            }
-        }
+        take_items(true);
 
         // ======================= service: every lane on a path has its rays back =======================
         // (BVH: the lanes whose two rays are done)
@@ -788,6 +800,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
         }
 
+#if RT_LATE_ITEMS
+        take_items(false);
+#endif
         SEC_MARK(4);
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
