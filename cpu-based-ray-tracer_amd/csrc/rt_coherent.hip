@@ -165,6 +165,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #endif
 // work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
 // more than one item per lane, so the launch tail stays one item long)
+#ifndef RT_BVH_DIV_FAST
+#define RT_BVH_DIV_FAST 0   // 1: the BVH variant divides with div_fast too (C5 -2.5 %)
+#endif
 #ifndef RT_LATE_ITEMS
 #define RT_LATE_ITEMS 1   // a lane whose item ended takes the next from the wave's pool in the same iteration (C4 +0.4 %, C5 +1.4 %)
 #endif
@@ -317,8 +320,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // the leaf-box variant divides with rt_device.h div_fast (y = the divisor's correctly rounded
     // reciprocal; C4 +1.1 %); the BVH variant keeps the IEEE division sequence (its register budget: C5
     // -2 % with div_fast)
-    auto sdiv = [](float x, float d, float y) { return BVH ? x / d : div_fast(x, d, y); };
-    auto vdiv = [](V3 a, float d, float y) { return BVH ? divs(a, d) : divs_fast(a, d, y); };
+    auto sdiv = [](float x, float d, float y) { return (BVH && !RT_BVH_DIV_FAST) ? x / d : div_fast(x, d, y); };
+    auto vdiv = [](V3 a, float d, float y) { return (BVH && !RT_BVH_DIV_FAST) ? divs(a, d) : divs_fast(a, d, y); };
     // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
     // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
     // pixel's samples in frame order (MC/Renderer.cpp:128-133).  The kernel issues no global load
@@ -711,7 +714,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const float4 mb = S.mats[2 * mat];
                         const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                         st3(VS_LD, vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
-                                             BVH ? 0.0f : rcp_f32(sd2)),
+                                             (BVH && !RT_BVH_DIV_FAST) ? 0.0f : rcp_f32(sd2)),
                                         Q.lpdf, Q.y_lpdf));   // Q.lpdf = 1.0f / light_area
                         dB = wl;
                         hasB = true;
@@ -819,7 +822,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             cy = cy * 2.0f - 1.0f;
             float tg[4];
             mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
+            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], (BVH && !RT_BVH_DIV_FAST) ? 0.0f : rcp_f32(tg[3])));
             float wd[4];
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
