@@ -15,4 +15,4 @@ for N in 2 4 8; do
     timeout -k 10 200 python3 -u tools/sweep_env.py --nranks $N --rank $R --set "" >> "$OUT/band_scaling.jsonl" 2>> "$OUT/band.err"
   done
 done
-timeout -k 10 600 python3 -u tools/cpu_reference_configs.py > "$OUT/cpu_reference_configs.jsonl" 2> "$OUT/cpu.err"
+[ "${SKIP_CPU:-0}" = "1" ] || timeout -k 10 600 python3 -u tools/cpu_reference_configs.py > "$OUT/cpu_reference_configs.jsonl" 2> "$OUT/cpu.err"
