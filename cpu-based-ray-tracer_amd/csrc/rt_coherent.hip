@@ -168,6 +168,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BVH_DIV_FAST
 #define RT_BVH_DIV_FAST 0   // 1: the BVH variant divides with div_fast too (C5 -2.5 %)
 #endif
+#ifndef RT_LIGHT_SKIP
+#define RT_LIGHT_SKIP 1   // NARROW: skip shadow-ray candidates coplanar with the sampled light triangle
+#endif
 #ifndef RT_LATE_ITEMS
 #define RT_LATE_ITEMS 1   // a lane whose item ended takes the next from the wave's pool in the same iteration (C4 +0.4 %, C5 +1.4 %)
 #endif
@@ -444,6 +447,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
+    uint32_t bskip = 0;                       // NARROW: shadow-ray candidates that cannot block (light plane)
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
     int triA = -1;                            // closest triangle
     bool occB = false;                        // shadow ray blocked
@@ -704,7 +708,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     hasB = false;
                     if (Q.has_light) {
                         V3 q, nl0;
-                        sample_light(S, Q.light_area, G, q, nl0);
+                        uint32_t lskip = 0;
+                        sample_light(S, Q.light_area, G, q, nl0, &lskip);
                         const V3 p2q = sub(q, p);
                         const V3 wl = glm_normalize(p2q);
                         const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
@@ -718,6 +723,10 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                                         Q.lpdf, Q.y_lpdf));   // Q.lpdf = 1.0f / light_area
                         dB = wl;
                         hasB = true;
+                        // triangles (near-)coplanar with the sampled light triangle are hit, if at all, within
+                        // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
+                        // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
+                        if (NARROW && !BVH && RT_LIGHT_SKIP) bskip = sc2 >= 0.25f ? lskip : 0u;
                     }
                     // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
                     cont = G.next() < Q.rr && depth < 4096u;
@@ -903,7 +912,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             for (; b < nb; ++b) one_box(bx[b]);
             if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb), "v"(ma), "v"(mb));
         }
-        if (NARROW) { ca = ma; cb = mb; }
+        if (NARROW) { ca = ma; cb = RT_LIGHT_SKIP ? (mb & ~bskip) : mb; }
         if (!trA || !fin) ca = 0;
         if (!trB || !fin) cb = 0;
         if (!fin && (trA || trB)) {
@@ -932,16 +941,17 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             const uint32_t tot = sec_w[15];
             SEC_COUNT(8, (tot + 63u) >> 6);
 #if RT_SECTIONS >= 2
-            // the wave's distinct candidate triangles: ray A's, ray B's, either (its own build: the loop
-            // is timed with the Moller-Trumbore section)
-            uint32_t ua = 0, ub = 0, uab = 0;
-            for (uint32_t t = 0; t < 64u; ++t) {
-                const bool a_ = __ballot(((ca >> t) & 1u) != 0u) != 0, b_ = __ballot(((cb >> t) & 1u) != 0u) != 0;
-                ua += a_ ? 1u : 0u; ub += b_ ? 1u : 0u; uab += (a_ || b_) ? 1u : 0u;
+            // candidate overlap of the lane's two rays (its own build: timed with the MT section):
+            // sum over lanes of |A & B|, and the wave's loop length per lane-candidate order --
+            // max |A| + |B| (one test per ray and candidate) vs max |A | B| (one pass per triangle)
+            uint32_t both = (uint32_t)__popcll(ca & cb), sep = (uint32_t)(__popcll(ca) + __popcll(cb)), uni = (uint32_t)__popcll(ca | cb);
+            SEC_SUM(16, both);
+            for (int off = 32; off >= 1; off >>= 1) {
+                sep = max(sep, (uint32_t)__shfl_xor((int)sep, off));
+                uni = max(uni, (uint32_t)__shfl_xor((int)uni, off));
             }
-            SEC_COUNT(16, ua);
-            SEC_COUNT(17, ub);
-            SEC_COUNT(18, uab);
+            SEC_COUNT(17, sep);
+            SEC_COUNT(18, uni);
 #endif
         }
 #endif

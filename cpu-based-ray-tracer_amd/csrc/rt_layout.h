@@ -21,7 +21,8 @@
 //  mats    : 2 x float4 per material: (brdf = albedo/PI, emitting), (emission, 0)
 //  lnodes  : light-mesh BVH for area sampling (BVH::Sampling_from_node, MC/BVH.h:114-129):
 //            1 x float4 per node (area, bits(left), bits(right), bits(light_tri)), root = 0
-//  ltris   : 4 x float4 per light triangle: (a, 0), (b, 0), (c, 0), (n, area)
+//  ltris   : 4 x float4 per light triangle: (a, skip), (b, 0), (c, 0), (n, area); skip: bits of the
+//            scene triangles (<= 32) a shadow ray toward this triangle cannot be blocked by (rt_scene.cpp)
 //  wmats   : Whitted-style shading (BVH Ray Tracer, BV/Renderer.cpp:172-229): 1 x float4 per
 //            material: (diffuse color, phong_diffuse)
 //  plights : point lights in insertion order (BV/LightSource.h, BV/Renderer.cpp:38-39):

@@ -595,6 +595,58 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             q[12] = t.n.x; q[13] = t.n.y; q[14] = t.n.z; q[15] = t.area;
         }
         out.hdr.light_area = mn[mesh_root[light]].area;
+        // Scenes of <= 32 triangles (the vertex kernel's narrow leaf-box build): per light triangle, the
+        // triangles no shadow ray toward a point q of it can be blocked by.  A triangle T whose vertices
+        // lie within eta of the light triangle's plane, with a normal parallel to it (|cos| >= 0.999) and
+        // no sliver corner at its first vertex (sin >= 0.1), meets a ray p -> q only within eta / |cos|
+        // of q; the kernel skips these candidates when |cos| >= 0.25 (rt_coherent.hip bskip), where the
+        // reference's t (mixed-precision Moller-Trumbore, MC/TriangleMesh.h:19-45) is within
+        // 5 * 2^-24 * (|o - a| + t) / (0.1 * 0.2) <= 3e-5 * extent of the true one.  So t > slen - 0.01 and
+        // `slen < t + 0.01f` (MC/Renderer.cpp:184) holds: T never occludes.  eta / 0.25 + 6e-5 * extent
+        // must stay below 0.008, else no mask is set.
+        if (NT <= 32) {
+            double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+            auto vert = [&](uint32_t s, int k, double v[3]) {
+                const float* q = &out.tris[16 * (size_t)s];
+                for (int a = 0; a < 3; ++a) v[a] = (double)q[a] + (k == 1 ? (double)q[4 + a] : k == 2 ? (double)q[8 + a] : 0.0);
+            };
+            for (uint32_t s = 0; s < NT; ++s)
+                for (int k = 0; k < 3; ++k) {
+                    double v[3];
+                    vert(s, k, v);
+                    for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], v[a]); hi[a] = std::max(hi[a], v[a]); }
+                }
+            const double extent = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) + (hi[2] - lo[2]) * (hi[2] - lo[2]));
+            const double eta = 0.0015;
+            if (eta / 0.25 + 6e-5 * extent <= 0.008) {
+                for (size_t k = 0; k < ltri_of.size(); ++k) {
+                    float* lq = &out.ltris[16 * k];
+                    double n[3] = {lq[12], lq[13], lq[14]};
+                    const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+                    if (!(nn > 0.0)) continue;
+                    for (int a = 0; a < 3; ++a) n[a] /= nn;
+                    const double d0 = n[0] * lq[0] + n[1] * lq[1] + n[2] * lq[2];
+                    uint32_t mask = 0;
+                    for (uint32_t s = 0; s < NT; ++s) {
+                        const float* q = &out.tris[16 * (size_t)s];
+                        bool near = true;
+                        for (int kk = 0; kk < 3 && near; ++kk) {
+                            double v[3];
+                            vert(s, kk, v);
+                            near = std::fabs(n[0] * v[0] + n[1] * v[1] + n[2] * v[2] - d0) <= eta;
+                        }
+                        const double e1[3] = {q[4], q[5], q[6]}, e2[3] = {q[8], q[9], q[10]};
+                        const double c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+                        const double l1 = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]), l2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
+                        const double lc = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+                        if (!near || !(lc >= 0.1 * l1 * l2) || !(lc > 0.0)) continue;
+                        if (std::fabs((c[0] * n[0] + c[1] * n[1] + c[2] * n[2]) / lc) < 0.999) continue;
+                        mask |= 1u << s;
+                    }
+                    std::memcpy(&lq[3], &mask, 4);
+                }
+            }
+        }
         const MaterialDesc& m = meshes_[light].material;
         out.hdr.light_emission[0] = m.emission.x; out.hdr.light_emission[1] = m.emission.y; out.hdr.light_emission[2] = m.emission.z;
     }
