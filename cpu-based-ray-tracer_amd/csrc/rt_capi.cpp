@@ -21,6 +21,10 @@ struct rt_scene {
     bool built = false;
 };
 
+// device counters: [0, 64) work / overflow / section counters, [64, 512) diagnostic histograms
+// (RT_SECTIONS >= 3 builds, rt_coherent.hip)
+static constexpr uint32_t kCounterWords = 512;
+
 struct rt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -406,7 +410,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess || hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev3) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, 512) != hipSuccess ||
+        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, kCounterWords * 8) != hipSuccess ||
         hipHostMalloc((void**)&c->h_ovf, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
@@ -604,6 +608,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0, coh_bvh) : rt_lane_state_lds_bytes(exact);
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
         P.lds_scene_quads -= 2 * P.n_lboxes + 2 * P.n_nodes;
+        P.lds_scene_quads += (RT_LDS_TRI_QUADS - 4) * P.n_tris;   // the padded triangle stride (rt_kernels.h)
     }
     if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; materials and the light
         // tables stay in LDS when they are small (C5: 21 quads)
@@ -649,7 +654,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const uint64_t px_local = (uint64_t)c->local_rows * c->W;
     const uint64_t items_px = P.n_items;   // 8x8-tile-padded pixel items
     c->last_flags = p->flags;
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, 512, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * 8, c->stream));
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
         if (whitted && c->hdr.n_went > 0) {
@@ -876,7 +881,7 @@ rt_status rt_synchronize(rt_ctx* c)
 
 rt_status rt_debug_counters(rt_ctx* c, uint64_t* out, uint32_t n)
 {
-    if (!c || !out || n > 64) return RT_ERR_INVALID;
+    if (!c || !out || n > kCounterWords) return RT_ERR_INVALID;
     HIPC(c, hipStreamSynchronize(c->stream));
     HIPC(c, hipMemcpy(out, c->d_counters, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return RT_OK;

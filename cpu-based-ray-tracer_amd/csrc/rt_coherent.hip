@@ -151,6 +151,20 @@ __device__ __forceinline__ bool box_hit_pk(const f2 sx, const f2 sy, const f2 sz
     return (tout >= 0.0f) && (tin <= tout);
 }
 
+// a triangle row for Moller-Trumbore: RT_TRI_B128 keeps the unused .w so the read is one ds_read_b128
+// (16-lane groups over 64 banks, 4 LDS cycles) instead of a ds_read_b96 (8-lane groups over 32 banks,
+// 8 cycles)
+#ifndef RT_TRI_B128
+#define RT_TRI_B128 0
+#endif
+__device__ __forceinline__ void tri_ld3(const float4* p, float4& t0, float4& t1, float4& t2)
+{
+    t0 = p[0]; t1 = p[1]; t2 = p[2];
+#if RT_TRI_B128
+    asm volatile("" : "+v"(t0.w), "+v"(t1.w), "+v"(t2.w));   // one wait for the three reads
+#endif
+}
+
 __device__ __forceinline__ V3 rcp3(V3 d) { return V3{rcp_f32(d.x), rcp_f32(d.y), rcp_f32(d.z)}; }
 __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
@@ -167,6 +181,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // more than one item per lane, so the launch tail stays one item long)
 #ifndef RT_BVH_DIV_FAST
 #define RT_BVH_DIV_FAST 0   // 1: the BVH variant divides with div_fast too (C5 -2.5 %)
+#endif
+#ifndef RT_MT_FLOAT
+#define RT_MT_FLOAT 0   // 1: leaf-box variant decides Moller-Trumbore in float, the double part only where needed (C4 -2.4 %)
 #endif
 #ifndef RT_LIGHT_SKIP
 #define RT_LIGHT_SKIP 1   // NARROW: skip shadow-ray candidates coplanar with the sampled light triangle
@@ -224,6 +241,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_MT_PREFETCH
 #define RT_MT_PREFETCH 0
 #endif
+#if RT_MT_PREFETCH && RT_MT_FLOAT
+#error "RT_MT_PREFETCH is an A/B of the double-precision loop: build it with RT_MT_FLOAT=0"
+#endif
 // Moller-Trumbore spread over the wave through an LDS (lane, candidate) pair list (A/B build; the host
 // sizes the list from RT_PAIR_CAP).  C4: 6209 -> 5294 Msamples/s (MT loop iterations 13.5 -> 5.6 per
 // trace step at 91 % lane use, but each chunk costs the list writes, 10 ds_bpermute and the hit
@@ -275,6 +295,7 @@ template <bool EXACT, bool BVH, bool NARROW>
 __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
+    constexpr uint32_t TQ = BVH ? 4u : (uint32_t)RT_LDS_TRI_QUADS;   // float4s per triangle in S.tris
     SceneView S;
     S.n_nodes = P.n_nodes;
     if (BVH) {
@@ -297,17 +318,19 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // are read with scalar loads)
         // (tris | mats | lnodes | ltris; the BVH nodes stay in HBM -- only a ray with a non-finite
         // reciprocal direction walks them -- and the leaf boxes are read with scalar loads)
+        // (triangles at a stride of TQ float4s: rt_kernels.h RT_LDS_TRI_QUADS)
         const uint32_t tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
         float4* dt = lds_scene;
-        float4* dm = dt + tq;
+        float4* dm = dt + TQ * P.n_tris;
         float4* dl = dm + mq;
         float4* dlt = dl + lq;
-        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[i] = P.tris[i];
+        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[(i >> 2) * TQ + (i & 3u)] = P.tris[i];
         for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
         for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
         for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
         __syncthreads();
         S.nodes = P.nodes; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt; S.lboxes = nullptr;
+        S.tq = TQ;
     }
 
     const uint32_t lane = __lane_id();
@@ -581,7 +604,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 bool ends = false;
                 if (in_path && (!BVH || (tiA >= NN && tiB >= NN))) {
                     bool em = false;
-                    if (triA >= 0) em = S.mats[2 * f2i(S.tris[4 * triA].w)].w != 0.0f;
+                    if (triA >= 0) em = S.mats[2 * f2i(S.tris[TQ * triA].w)].w != 0.0f;
                     ends = triA < 0 || em || (pend && !cont);
                 }
                 if (ends) drain_all(dleft);
@@ -615,7 +638,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 // BVH variant: the material came with the hit (tri_mat)
                 mat = (BVH && RT_HIT_MAT == 1) ? (triA >> 24)
                     : (BVH && RT_HIT_MAT == 2) ? (int)lsu(P.has_light ? VS_HMAT_LIT : VS_HMAT_UNLIT)
-                                               : f2i(S.tris[4 * (BVH ? (triA & 0xFFFFFF) : triA)].w);
+                                               : f2i(S.tris[TQ * (BVH ? (triA & 0xFFFFFF) : triA)].w);
                 emissive = S.mats[2 * mat].w != 0.0f;
             }
             bool vertex = false;
@@ -701,7 +724,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
                 const int ti3 = (BVH && RT_HIT_MAT == 1) ? (triA & 0xFFFFFF) : triA;
-                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[4 * ti3 + 3];
+                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[TQ * ti3 + 3];
                 const V3 wo = neg(dA);
                 const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
                 const V3 N{tq3.x, tq3.y, tq3.z};
@@ -875,7 +898,11 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // ======================= trace both rays of every lane =======================
         if (!BVH) {
         const bool trA = in_path && hasA, trB = in_path && hasB;
+#if RT_MT_FLOAT
+        triA = -1; occB = false;   // tA is formed after the Moller-Trumbore loop
+#else
         tA = 1.7976931348623157e308; triA = -1; occB = false;
+#endif
         // the reciprocal directions are computed here, not when the rays are set up: they are then
         // temporaries of the box loop instead of 6 registers live across the iteration
         rA = rcp3(dA); rB = rcp3(dB);
@@ -928,6 +955,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             if (trA) {
                 const Ray r{o, dA, rA, dA.x < 0.0f, dA.y < 0.0f, dA.z < 0.0f};
                 bool dummy = false;
+                tA = 1.7976931348623157e308;
                 traverse_impl<false, false>(S, r, false, 0.0, tA, triA, dummy, nt, tt);
             }
             if (trB) {
@@ -960,14 +988,95 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             SEC_COUNT(17, sep);
             SEC_COUNT(18, uni);
 #endif
+#if RT_SECTIONS >= 3
+            {   // candidate histograms (global atomics; diagnostic builds only): [64 + n] lanes with n ray-A
+                // candidates, [128 + n] with n ray-B candidates, [192 + n] trace steps whose busiest lane
+                // has n, [256 + tri] / [288 + tri] ray A / ray B candidates by triangle
+                unsigned long long* hc = (unsigned long long*)kargs4().counters;
+                const uint32_t na = (uint32_t)__popcll(ca), nbb = (uint32_t)__popcll(cb);
+                if (trA && fin) atomicAdd(&hc[64 + na], 1ull);
+                if (trB && fin) atomicAdd(&hc[128 + nbb], 1ull);
+                uint32_t mx = na + nbb;
+                for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+                if (sec_first()) atomicAdd(&hc[192 + (mx < 63u ? mx : 63u)], 1ull);
+                for (uint64_t m = ca; m != 0; m &= m - 1) atomicAdd(&hc[256 + (__builtin_ctzll(m) & 31)], 1ull);
+                for (uint64_t m = cb; m != 0; m &= m - 1) atomicAdd(&hc[288 + (__builtin_ctzll(m) & 31)], 1ull);
+                // the wave's union of candidate triangles: [400] ray A, [401] ray B, [402] either, [403] trace steps
+                uint32_t oa = (uint32_t)ca, ob = (uint32_t)cb;
+                for (int off = 32; off >= 1; off >>= 1) { oa |= (uint32_t)__shfl_xor((int)oa, off); ob |= (uint32_t)__shfl_xor((int)ob, off); }
+                if (sec_first()) {
+                    atomicAdd(&hc[400], (unsigned long long)__popc(oa)); atomicAdd(&hc[401], (unsigned long long)__popc(ob));
+                    atomicAdd(&hc[402], (unsigned long long)__popc(oa | ob)); atomicAdd(&hc[403], 1ull);
+                }
+            }
+#endif
         }
 #endif
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
         auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
+#if RT_MT_FLOAT
+            // Moller-Trumbore decided in float where the float values decide it (rt_device.h mt_float);
+            // the closest hit is kept as its triangle and q = tn * rcp(den) (relative error < 2^-22), which
+            // orders the hits; its t = (double)tn * rcp_f64_of_f32(den) is formed once, after the loop, from
+            // the float part recomputed for that triangle (the same operations: the same tn, den)
+            float tnA = 0.0f, denA = 1.0f;
+            auto t_of = [](float tn, float den) { return (double)tn * rcp_f64_of_f32(den); };
             auto test = [&](const bool useA, const int tri, uint64_t& rest) {
                 const V3 d = useA ? dA : dB;
-                const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
+                float4 t0, t1, t2;
+                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
+                float tn, den, b2n, b3n;
+                const int c = mt_float(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, tn, den, b2n, b3n);
+#if RT_SECTIONS
+                SEC_COUNT(5, 1u);
+                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+                SEC_COUNT(12, (uint32_t)__popcll(__ballot(useA)));
+                SEC_COUNT(14, (uint32_t)__popcll(__ballot(c != MT_MISS)));
+                SEC_COUNT(19, (uint32_t)__popcll(__ballot(c == MT_OPEN)));
+#endif
+                if (c == MT_MISS) return;
+                double t = 0.0;
+                float q;
+                if (c == MT_OPEN) {   // rare: the barycentric boundary within 1e-5, or badly scaled operands
+                    if (!mt_open(tn, den, b2n, b3n, t)) return;
+                    q = (float)t;
+                } else {
+                    q = tn * __builtin_amdgcn_rcpf(den);   // v_rcp_f32: 1 ulp; den, tn in [2^-40, 2^40]
+                }
+                if (useA) {
+                    // the reference's `t <= tA` (MC/BVH.h:97-100: the later leaf wins a tie), decided by q
+                    // outside a 2^-19 band around qA (q, qA within 2^-22 of t, tA when both are normal
+                    // -- an MT_OPEN hit or best is compared exactly)
+                    const float qA = tnA * __builtin_amdgcn_rcpf(denA);
+                    bool take;
+                    if (triA < 0) take = true;
+                    else if (c == MT_HIT && q < qA * (1.0f - 0x1p-19f)) take = true;
+                    else if (c == MT_HIT && q > qA * (1.0f + 0x1p-19f)) take = false;
+                    else take = (c == MT_OPEN ? t : t_of(tn, den)) <= t_of(tnA, denA);
+                    if (take) { tnA = tn; denA = den; triA = tri; }
+                } else {
+                    // blocking: !(slen < t + 0.01f) (MC/Renderer.cpp:184), decided by q + 0.01f outside a
+                    // 2^-18 band around slen
+                    const float s = q + 0.01f;
+                    bool blk;
+                    if (c == MT_HIT && s > slen * (1.0f + 0x1p-18f)) blk = false;
+                    else if (c == MT_HIT && s < slen * (1.0f - 0x1p-18f)) blk = true;
+                    else blk = !((double)slen < (c == MT_OPEN ? t : t_of(tn, den)) + (double)0.01f);
+                    if (blk) {
+                        occB = true;
+                        rest = 0;   // B's candidates come last: nothing else to test
+                    }
+                }
+            };
+            // (a lane that walked the BVH -- non-finite reciprocal -- has its walk's tA)
+            auto finish_mt = [&]() { if (fin) tA = t_of(tnA, denA); };
+#else
+            auto finish_mt = [&]() {};
+            auto test = [&](const bool useA, const int tri, uint64_t& rest) {
+                const V3 d = useA ? dA : dB;
+                float4 t0, t1, t2;
+                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
                 double t;
                 const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
 #if RT_SECTIONS
@@ -985,17 +1094,18 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     }
                 }
             };
+#endif
             if (NARROW && RT_MT_PREFETCH) {
                 // the next candidate's triangle is read from LDS before the current one is tested
                 uint64_t cm = ca | (cb << 32);
                 if (cm != 0) {
                     uint32_t bit = (uint32_t)__builtin_ctzll(cm);
                     cm &= cm - 1;
-                    const float4* T = S.tris + 4 * (bit & 31u);
+                    const float4* T = S.tris + TQ * (bit & 31u);
                     float4 u0 = T[0], u1 = T[1], u2 = T[2];
                     for (;;) {
                         const uint32_t nbit = cm != 0 ? (uint32_t)__builtin_ctzll(cm) : bit;
-                        const float4* N = S.tris + 4 * (nbit & 31u);
+                        const float4* N = S.tris + TQ * (nbit & 31u);
                         const float4 n0 = N[0], n1 = N[1], n2 = N[2];
                         const bool useA = bit < 32u;
                         double t;
@@ -1030,6 +1140,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     test(useA, tri, cb);
                 }
             }
+            finish_mt();
         };
         for (int rep = 1; rep < RT_REP_MT; ++rep) {   // cost-attribution builds only: results discarded
             uint64_t xa = ca, xb = cb;
@@ -1085,7 +1196,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     double t = 0.0;
                     bool hit = false;
                     if (valid) {
-                        const float4 t0 = S.tris[4 * tri], t1 = S.tris[4 * tri + 1], t2 = S.tris[4 * tri + 2];
+                        float4 t0, t1, t2;
+                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
                         hit = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, po, pd, t);
                     }
                     // this lane's pairs in the chunk: positions [s, s + n)
@@ -1114,6 +1226,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         } else {
             mt_loop(ca, cb, tA, triA, occB);
         }
+#if RT_SECTIONS >= 3
+        {   // [320 + tri] ray A's closest hits by triangle, [352] blocked ray-B lanes (fin lanes)
+            unsigned long long* hc = (unsigned long long*)kargs4().counters;
+            if (trA && fin && triA >= 0) atomicAdd(&hc[320 + (triA & 31)], 1ull);
+            if (trB && fin && occB) atomicAdd(&hc[352], 1ull);
+        }
+#endif
         } else {
             // BVH rounds (the megakernel's, rt_kernels.hip): `steps` box tests per round on the lane's
             // current ray (A until it is done, then B), up to two leaves postponed in DFS order and
@@ -1195,7 +1314,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                             e1 = sub(V3{t1.x, t1.y, t1.z}, va);
                             e2 = sub(V3{t2.x, t2.y, t2.z}, va);
                         } else {
-                            const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
+                            const float4 t0 = S.tris[TQ * pk], t1 = S.tris[TQ * pk + 1], t2 = S.tris[TQ * pk + 2];
                             va = V3{t0.x, t0.y, t0.z}; e1 = V3{t1.x, t1.y, t1.z}; e2 = V3{t2.x, t2.y, t2.z};
                             pmat = f2i(t0.w);
                         }

@@ -1,6 +1,14 @@
 // rt_kernels.h -- launch interface between the C-ABI layer (rt_capi.cpp) and the HIP kernels.
 #ifndef RT_KERNELS_H
 #define RT_KERNELS_H
+
+// float4s per triangle in the leaf-box vertex kernel's LDS copy of the triangles (A/B knob): 5 (one pad)
+// puts the triangles of a 16-lane ds_read_b128 group on 16 different bank phases (20 dwords apart, mod
+// 64) instead of 4 (16 dwords apart).  C4: 6861 (4) vs 6869 (5, ds_read_b96) vs 6839 (5, ds_read_b128)
+// Msamples/s -- the bank conflicts do not bind
+#ifndef RT_LDS_TRI_QUADS
+#define RT_LDS_TRI_QUADS 4
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

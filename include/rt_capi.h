@@ -206,9 +206,9 @@ typedef struct {
 #define RT_KERNEL_WHITTED 2   /* whitted_kernel / whitted_world_kernel (rt_whitted.hip) */
 #define RT_KERNEL_VERTEX_BVH 3   /* pt_coherent_kernel's BVH variant (rt_coherent.hip): other path scenes */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
-/* diagnostic: the raw device counters of the last rt_render (up to 64 x u64; [16..23] = wave cycles per
- * section and [24..39] = wave-level event counts of the vertex kernel in RT_SECTIONS builds), after a
- * stream synchronisation */
+/* diagnostic: the raw device counters of the last rt_render (up to 512 x u64; [16..23] = wave cycles per
+ * section and [24..43] = wave-level event counts of the vertex kernel in RT_SECTIONS builds, [64..511]
+ * candidate histograms in RT_SECTIONS >= 3 builds), after a stream synchronisation */
 rt_status rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
 
 /* ------------------------------------------------------------------ several GPUs, one frame

@@ -5,6 +5,7 @@ comparing builds (profiles/run_rocprof.sh profiles bench.py itself).
     rocprofv3 --pmc SQ_INSTS_VALU -- python3 tools/prof_one.py librt_hip.so --spp 64
 """
 import argparse
+import json
 import importlib.util
 import os
 
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--sections", action="store_true", help="print the wave-cycle split of an RT_SECTIONS build")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    ap.add_argument("--hist", action="store_true", help="print the candidate histograms of an RT_SECTIONS=3 build")
     ap.add_argument("--reps", type=int, default=1, help="measured renders after the warm-up")
     args = ap.parse_args()
     spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(PKG, "__init__.py"))
@@ -54,8 +56,16 @@ def main():
                "pairsA/it": round(n[13] / it, 2), "mt_lanesA/it": round(n[12] / it, 2), "mt_hits/it": round(n[14] / it, 2),
                "fin_iters_with_drain/it": round(n[9] / it, 3), "fin_lanes_with_drain/it": round(n[10] / it, 3),
                "drain_lanes_top/it": round(n[11] / it, 2),
-               "union_tris_A/it": round(n[16] / it, 2), "union_tris_B/it": round(n[17] / it, 2), "union_tris_AB/it": round(n[18] / it, 2),
+               "union_tris_A/it": round(n[16] / it, 2), "union_tris_B/it": round(n[17] / it, 2), "union_tris_AB/it": round(n[18] / it, 2), "mt_open/it": round(n[19] / it, 4),
                "lane_iterations_per_sample": round(n[0] * 64 / samples, 3)})
+    if args.hist:
+        h = c.debug_counters(512)
+        tot = lambda a, b: sum(h[a:b])
+        out = {"A_candidates_hist": h[64:128], "B_candidates_hist": h[128:192], "wave_max_hist": h[192:256],
+               "A_cand_by_tri": h[256:288], "B_cand_by_tri": h[288:320], "A_closest_by_tri": h[320:352], "B_blocked": h[352],
+               "A_rays": tot(64, 128), "B_rays": tot(128, 192),
+               "wave_union_A": h[400] / max(h[403], 1), "wave_union_B": h[401] / max(h[403], 1), "wave_union_AB": h[402] / max(h[403], 1)}
+        print(json.dumps(out))
     c.close()
 
 
