@@ -118,6 +118,9 @@ def lib():
         "rt_destroy": (None, [vp]),
         "rt_last_error": (C.c_char_p, [vp]),
         "rt_upload_scene": (i32, [vp, vp]),
+        "rt_upload_scene_gpu_bvh": (i32, [vp, vp, fp]),
+        "rt_scene_lbvh_host": (i32, [vp, fp, fp]),
+        "rt_debug_scene_arrays": (i32, [vp, fp, u32, fp, u32]),
         "rt_resize": (i32, [vp, u32, u32, u32, u32, u32]),
         "rt_local_rows": (u32, [vp]),
         "rt_render": (i32, [vp, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(u32), fp]),
@@ -276,6 +279,14 @@ class Scene:
         i = SceneInfo()
         self._check(lib().rt_scene_get_info(self.h, C.byref(i)), "rt_scene_get_info")
         return i
+
+    def lbvh_host(self):
+        """The device build's tree, built on the host (rt_scene_lbvh_host): nodes (2n-1, 8) and triangle
+        records (n, 16) as float32 arrays in the traversal layout."""
+        n = self.info().n_tris
+        nodes = np.zeros((2 * n - 1, 8), np.float32); tris = np.zeros((n, 16), np.float32)
+        self._check(lib().rt_scene_lbvh_host(self.h, _fp(nodes), _fp(tris)), "rt_scene_lbvh_host")
+        return nodes, tris
 
     def export(self):
         i = self.info()
@@ -481,6 +492,18 @@ class Context:
 
     def upload(self, scene):
         self._check(lib().rt_upload_scene(self.h, scene.h), "rt_upload_scene")
+
+    def upload_gpu_bvh(self, scene):
+        """rt_upload_scene_gpu_bvh: the BVH built on the device (non-parity fast path); returns the build ms."""
+        ms = C.c_float(0.0)
+        self._check(lib().rt_upload_scene_gpu_bvh(self.h, scene.h, C.byref(ms)), "rt_upload_scene_gpu_bvh")
+        return ms.value
+
+    def debug_scene_arrays(self, n_nodes, n_tris):
+        """The device's node (n_nodes, 8) and triangle (n_tris, 16) arrays (rt_debug_scene_arrays)."""
+        nodes = np.zeros((n_nodes, 8), np.float32); tris = np.zeros((n_tris, 16), np.float32)
+        self._check(lib().rt_debug_scene_arrays(self.h, _fp(nodes), nodes.size, _fp(tris), tris.size), "rt_debug_scene_arrays")
+        return nodes, tris
 
     def resize(self, W, H, band=8, rank=0, nranks=1):
         self._check(lib().rt_resize(self.h, W, H, band, rank, nranks), "rt_resize")

@@ -488,6 +488,77 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     return RT_OK;
 }
 
+namespace {
+// the LBVH build's inputs from a built scene: the vertices (9 floats) and the records (16 floats) of each
+// triangle, in the host tree's DFS order (the build's order does not depend on it)
+bool lbvh_inputs(const rt_scene* s, std::vector<float>& verts)
+{
+    const uint32_t n = s->flat.hdr.n_tris;
+    if (n < 2 || s->flat.dbg_tri_f.size() < 13 * (size_t)n || s->flat.tris.size() < 16 * (size_t)n) return false;
+    verts.resize(9 * (size_t)n);
+    for (uint32_t i = 0; i < n; ++i) std::memcpy(&verts[9 * (size_t)i], &s->flat.dbg_tri_f[13 * (size_t)i], 9 * sizeof(float));
+    return true;
+}
+}  // namespace
+
+rt_status rt_scene_lbvh_host(const rt_scene* s, float* nodes, float* tris)
+{
+    if (!s || !nodes || !tris) return RT_ERR_INVALID;
+    if (!s->built) return RT_ERR_STATE;
+    std::vector<float> verts, nv, tv;
+    if (!lbvh_inputs(s, verts)) return RT_ERR_INVALID;
+    if (!lbvh_build_host(s->flat.hdr.n_tris, verts.data(), s->flat.tris.data(), nv, tv)) return RT_ERR_INVALID;
+    std::memcpy(nodes, nv.data(), nv.size() * sizeof(float));
+    std::memcpy(tris, tv.data(), tv.size() * sizeof(float));
+    return RT_OK;
+}
+
+rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
+{
+    if (!c || !s) return RT_ERR_INVALID;
+    if (!s->built) { c->err = "scene not built (rt_scene_build)"; return RT_ERR_STATE; }
+    std::vector<float> verts;
+    if (!lbvh_inputs(s, verts)) { c->err = "the GPU BVH build needs >= 2 triangles"; return RT_ERR_INVALID; }
+    rt_status r = rt_upload_scene(c, s);   // materials, light tables, ... (the host tree is replaced below)
+    if (r != RT_OK) return r;
+    const uint32_t n = s->flat.hdr.n_tris, m = 2 * n - 1;
+    float* d_verts = nullptr;
+    float4 *d_nodes = nullptr, *d_tris = nullptr;
+    auto fail = [&](hipError_t e) { dfree(d_verts); dfree(d_nodes); dfree(d_tris); return hip_fail(c, e, "rt_upload_scene_gpu_bvh"); };
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_verts, verts.size() * sizeof(float))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc((void**)&d_nodes, 2 * (size_t)m * sizeof(float4))) != hipSuccess) return fail(e);
+    if ((e = hipMalloc((void**)&d_tris, 4 * (size_t)n * sizeof(float4))) != hipSuccess) return fail(e);
+    if ((e = hipMemcpy(d_verts, verts.data(), verts.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
+    if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return fail(e);
+    if ((e = lbvh_build_device(n, d_verts, c->d_tris, d_nodes, d_tris, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return fail(e);
+    float ms = 0.0f;
+    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    if (build_ms) *build_ms = ms;
+    dfree(d_verts);
+    dfree(c->d_nodes); dfree(c->d_tris);
+    c->d_nodes = d_nodes; c->d_tris = d_tris;
+    // the BVH-walking kernels: no leaf-box table, no compact tree
+    dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
+    c->hdr.n_nodes = m;
+    c->hdr.n_lboxes = 0;
+    c->hdr.has_qnodes = 0;
+    return RT_OK;
+}
+
+rt_status rt_debug_scene_arrays(rt_ctx* c, float* nodes, uint32_t n_node_floats, float* tris, uint32_t n_tri_floats)
+{
+    if (!c) return RT_ERR_INVALID;
+    if (!c->has_scene) return RT_ERR_STATE;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const size_t nn = std::min<size_t>(n_node_floats, 8 * (size_t)c->hdr.n_nodes), nt = std::min<size_t>(n_tri_floats, 16 * (size_t)c->hdr.n_tris);
+    if (nodes && nn) HIPC(c, hipMemcpy(nodes, c->d_nodes, nn * sizeof(float), hipMemcpyDeviceToHost));
+    if (tris && nt) HIPC(c, hipMemcpy(tris, c->d_tris, nt * sizeof(float), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 rt_status rt_resize(rt_ctx* c, uint32_t W, uint32_t H, uint32_t band, uint32_t rank, uint32_t nranks)
 {
     if (!c || W == 0 || H == 0 || band == 0 || nranks == 0 || rank >= nranks) return RT_ERR_INVALID;

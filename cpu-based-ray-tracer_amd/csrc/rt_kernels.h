@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 struct KParams {
     // scene (rt_layout.h)
     const float4* nodes; uint32_t n_nodes;
@@ -119,5 +121,11 @@ struct DenoiseParams {
     float prev_proj[16], prev_view[16];
 };
 hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream);
+
+// GPU BVH build (rt_lbvh.hip): a Karras LBVH in the traversal layout (rt_layout.h nodes / tris).
+// verts: 9 floats per triangle (a, b, c); recs: the triangle records (4 float4 per triangle); n >= 2.
+hipError_t lbvh_build_device(uint32_t n, const float* verts, const float4* recs, float4* nodes, float4* tris, hipStream_t s);
+// the same tree built on the host, sequentially (tests): 8 floats per node (2n - 1), 16 per triangle
+bool lbvh_build_host(uint32_t n, const float* verts, const float* recs, std::vector<float>& nodes, std::vector<float>& tris);
 
 #endif

@@ -109,6 +109,10 @@ rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 /* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node
  * (left right tri mesh top_level), tri_f 13/tri (a b c n area), tri_i 2/tri (mesh material) */
 rt_status rt_scene_export(const rt_scene* s, float* node_f, int32_t* node_i, float* tri_f, int32_t* tri_i);
+/* The scene's BVH built on the HOST in the device build's algorithm (tests of rt_upload_scene_gpu_bvh):
+ * a Karras LBVH over the Morton codes of the triangle-box centroids, one triangle per leaf, in the
+ * traversal layout -- nodes: 8 floats x (2 n_tris - 1), tris: 16 floats x n_tris.  Needs >= 2 triangles. */
+rt_status rt_scene_lbvh_host(const rt_scene* s, float* nodes, float* tris);
 
 /* ------------------------------------------------------------------ camera (host math) */
 typedef struct {
@@ -137,6 +141,16 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg);
 void rt_destroy(rt_ctx* ctx);
 const char* rt_last_error(const rt_ctx* ctx);
 rt_status rt_upload_scene(rt_ctx* ctx, const rt_scene* s);
+/* rt_upload_scene with the BVH built on the DEVICE (rt_lbvh.hip, a non-parity fast path for large
+ * meshes; the reference builds on the host, MC/BVH.h:131-214): a Karras linear BVH over 30-bit Morton
+ * codes, one triangle per leaf, written in DFS order with skip pointers.  Closest-hit t values equal the
+ * reference-tree render's (the Moller-Trumbore operations do not depend on the tree); a tie between two
+ * triangles at one t resolves by this tree's DFS order instead of the reference's.  Renders use the
+ * BVH-walking kernels (no leaf-box table).  build_ms (may be NULL) receives the build time on the
+ * device.  Needs >= 2 triangles. */
+rt_status rt_upload_scene_gpu_bvh(rt_ctx* ctx, const rt_scene* s, float* build_ms);
+/* diagnostic: copy the device's node / triangle arrays (up to n_node_floats / n_tri_floats floats) */
+rt_status rt_debug_scene_arrays(rt_ctx* ctx, float* nodes, uint32_t n_node_floats, float* tris, uint32_t n_tri_floats);
 /* full image size; allocates the accumulation (float4) and RGBA8 buffers for this device's pixels.
  * Pixels are dealt in row bands of `band` rows round-robin over `nranks` (band=8, rank=0, nranks=1
  * for one GPU); rt_local_rows() returns how many rows this device owns. */
