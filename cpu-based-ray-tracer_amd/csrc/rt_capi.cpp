@@ -84,7 +84,7 @@ struct rt_ctx {
     // frame chunking (KParams::n_chunks): split when a launch has fewer than min_px_per_lane pixels
     // per lane, into about items_per_lane items per lane but no chunk shorter than min_chunk_frames
     // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
-    uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 16;
+    uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 8;
     uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch; C4 needs 25 GB of 288
     bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(32 GB, 3/4 of free memory) per render
     float* d_lbuf = nullptr;
