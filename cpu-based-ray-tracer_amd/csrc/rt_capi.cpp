@@ -519,6 +519,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     if (!s->built) { c->err = "scene not built (rt_scene_build)"; return RT_ERR_STATE; }
     std::vector<float> verts;
     if (!lbvh_inputs(s, verts)) { c->err = "the GPU BVH build needs >= 2 triangles"; return RT_ERR_INVALID; }
+    if (s->flat.hdr.n_tris >= (1u << 30)) { c->err = "the GPU BVH build takes < 2^30 triangles (node ids are int)"; return RT_ERR_INVALID; }
     rt_status r = rt_upload_scene(c, s);   // materials, light tables, ... (the host tree is replaced below)
     if (r != RT_OK) return r;
     const uint32_t n = s->flat.hdr.n_tris, m = 2 * n - 1;
