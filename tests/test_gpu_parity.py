@@ -146,6 +146,18 @@ def test_matches_oracle_at_larger_size(ctx):
     assert e < RMSE_TOL and same == 1.0
 
 
+@pytest.mark.parametrize("rr", [0.5, 0.8, 0.9])
+def test_roulette_settings_match_oracle(ctx, rr):
+    """The reference UI's three Russian-roulette survival probabilities (MC/mainloop.cpp:96-110) on a
+    256x192x32 frame against the CPU restatement: bitwise accumulation and RGBA8 (at 0.9 paths average
+    ten vertices, so the fold ring and its drain run deep)."""
+    W, H, spp = 256, 192, 32
+    rgba, acc = render(ctx, W, H, spp, seed=3, rr=rr)
+    oacc, orgba, _ = O.Scene().render(W, H, spp, seed=3, rr=rr, threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(bits(acc), bits(oacc))
+    assert np.array_equal(rgba, orgba)
+
+
 def test_counters_and_no_stack_overflow(ctx):
     ctx.resize(64, 64)
     cam, _, _ = rt.camera_default(64, 64)
