@@ -92,10 +92,6 @@ struct rt_ctx {
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
-    // vertex kernel, leaf-box variant: entries per wave of the LDS (lane, candidate) pair list that spreads
-    // Moller-Trumbore over the wave in an RT_MT_COMPACT=1 build (RT_PAIR_CAP: -1 = as many as fit without
-    // costing occupancy, 0 = none: the per-lane loop, the default)
-    int pair_cap_force = 0;
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
@@ -385,7 +381,6 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_PAIR_CAP")) c->pair_cap_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = std::getenv("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
@@ -680,7 +675,6 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0, coh_bvh) : rt_lane_state_lds_bytes(exact);
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
         P.lds_scene_quads -= 2 * P.n_lboxes + 2 * P.n_nodes;
-        P.lds_scene_quads += (RT_LDS_TRI_QUADS - 4) * P.n_tris;   // the padded triangle stride (rt_kernels.h)
     }
     if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; materials and the light
         // tables stay in LDS when they are small (C5: 21 quads)
@@ -702,24 +696,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
     size_t shmem = ((lds || coh_bvh) ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
-    P.pair_cap = 0;
-    if (coh_box) {
-        // the pair list of the wave-spread Moller-Trumbore: as long as it costs no occupancy (a shorter list
-        // only means more windows per trace step), at least 64 entries
-        const size_t waves = c->block / 64;
-        auto list_bytes = [&](uint32_t cap) { return (waves * cap * sizeof(uint16_t) + 15) & ~(size_t)15; };
-        uint32_t cap = 0;
-        if (c->pair_cap_force >= 0) cap = std::min<uint32_t>((uint32_t)c->pair_cap_force, 4096u);
-        else
-            for (uint32_t k = 4096; k >= 64; k -= 32)
-                if (occupancy(shmem + list_bytes(k)) >= bpc) { cap = k; break; }
-        if (cap > 0) {
-            P.pair_cap = cap;
-            shmem += list_bytes(cap);
-            bpc = occupancy(shmem);
-        }
-    }
-    c->stats.pair_cap = P.pair_cap;
+    c->stats.pair_cap = 0;
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes

@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rt_device.h"
 #include "rt_kernels.h"
 #include "rt_path.h"
@@ -50,9 +52,7 @@ enum : uint32_t {
     VS_THR = 8, VS_LSUM = 11,            // FAST: throughput, radiance
     VS_WORDS_EXACT = 15, VS_WORDS_FAST = 14,
     VS_RNG = 15,                         // unlit scenes only: the Philox block of the current 4 draws
-    VS_WORDS_UNLIT = 19,
-    // BVH variant (RT_HIT_MAT 2): the closest hit's material, one word after the scene's lane state
-    VS_HMAT_LIT = 15, VS_HMAT_UNLIT = 19
+    VS_WORDS_UNLIT = 19
 };
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
@@ -117,10 +117,6 @@ struct VertexRng {
 // the three sign bits of the direct term (one 16-byte load instead of two)
 __device__ __forceinline__ void ring_load(const CKParams& Q, size_t at, float4& e, int& m)
 {
-#if RT_DIAG_NO_RING_LOAD
-    // cost attribution only (wrong images): the ring loads replaced by a value derived from the address
-    e = make_float4(0.1f, 0.1f, 0.1f, (float)(at & 7u) * 0.1f); m = 1; return;
-#endif
     e = Q.stack_ld[at];
     if (Q.ring_pack) {
         const uint32_t x = __float_as_uint(e.x), y = __float_as_uint(e.y), z = __float_as_uint(e.z);
@@ -151,20 +147,6 @@ __device__ __forceinline__ bool box_hit_pk(const f2 sx, const f2 sy, const f2 sz
     return (tout >= 0.0f) && (tin <= tout);
 }
 
-// a triangle row for Moller-Trumbore: RT_TRI_B128 keeps the unused .w so the read is one ds_read_b128
-// (16-lane groups over 64 banks, 4 LDS cycles) instead of a ds_read_b96 (8-lane groups over 32 banks,
-// 8 cycles)
-#ifndef RT_TRI_B128
-#define RT_TRI_B128 0
-#endif
-__device__ __forceinline__ void tri_ld3(const float4* p, float4& t0, float4& t1, float4& t2)
-{
-    t0 = p[0]; t1 = p[1]; t2 = p[2];
-#if RT_TRI_B128
-    asm volatile("" : "+v"(t0.w), "+v"(t1.w), "+v"(t2.w));   // one wait for the three reads
-#endif
-}
-
 __device__ __forceinline__ V3 rcp3(V3 d) { return V3{rcp_f32(d.x), rcp_f32(d.y), rcp_f32(d.z)}; }
 __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
@@ -173,115 +155,43 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // minimum waves per SIMD the register allocation must admit: 8 = at most 64 VGPRs (no VGPR spill; a
 // few SGPRs spill to VGPR lanes) and 78 SGPRs, so 8 blocks of 256 lanes are resident per CU -- the
 // hardware admits min(8, 800 / (ceil(sgpr / 16) * 16 + 16)) blocks (MI355X_MICROARCH.md, Residency),
-// one fewer than the occupancy API at 82-96 SGPRs -- with 15 LDS words per lane (+1-2 % over 7)
+// one fewer than the occupancy API at 82-96 SGPRs -- with 15 LDS words per lane (+1-2 % over 7; 7 / 6
+// waves: C4 +0.2 % / -1.9 %, profiles/r02/ab/ab_waves_per_simd_*)
 #ifndef RT_COH_MIN_WAVES
 #define RT_COH_MIN_WAVES 8
 #endif
-// work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
-// more than one item per lane, so the launch tail stays one item long)
-#ifndef RT_BVH_DIV_FAST
-#define RT_BVH_DIV_FAST 0   // 1: the BVH variant divides with div_fast too (C5 -2.5 %)
+// the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
+#ifndef RT_COH_BVH_MIN_WAVES
+#define RT_COH_BVH_MIN_WAVES 8
 #endif
-#ifndef RT_MT_FLOAT
-#define RT_MT_FLOAT 0   // 1: leaf-box variant decides Moller-Trumbore in float, the double part only where needed (C4 -2.4 %)
-#endif
-#ifndef RT_LIGHT_SKIP
-#define RT_LIGHT_SKIP 1   // NARROW: skip shadow-ray candidates coplanar with the sampled light triangle
-#endif
-#ifndef RT_ZERO_LD_SKIP
-#define RT_ZERO_LD_SKIP 1   // no shadow ray for a vertex whose unoccluded direct term is zero
-#endif
-#ifndef RT_LATE_ITEMS
-#define RT_LATE_ITEMS 1   // a lane whose item ended takes the next from the wave's pool in the same iteration (C4 +0.4 %, C5 +1.4 %)
-#endif
-#ifndef RT_HIT_MAT
-#define RT_HIT_MAT 0   // BVH variant, the closest hit's material kept 1: beside its index, 2: in an LDS word (C5 -1.5 % / -2.4 %: spills)
-#endif
-#ifndef RT_PARK_NT
-#define RT_PARK_NT 0   // 1: parked samples with non-temporal stores (A/B)
-#endif
-#ifndef WQ_BATCH
-#define WQ_BATCH 64u
-#endif
-// cost attribution (A/B builds, tools/ab_libs.py): run the leaf-box loop / the Moller-Trumbore loop
-// this many times per trace step (extra runs' results are discarded; the image is unchanged)
-#ifndef RT_REP_BOX
-#define RT_REP_BOX 1
-#endif
-#ifndef RT_REP_MT
-#define RT_REP_MT 1
-#endif
-// section timing (diagnostic builds): wave cycles spent in fold drain (top) / vertex / finish / work queue +
+// section timing (diagnostic builds, tools/prof_one.py --sections / --hist; compiled by
+// tests/test_build_variants.py): wave cycles spent in fold drain (top) / vertex / finish / work queue +
 // service head / camera / box loop / Moller-Trumbore, summed into counters[16..23]
 #ifndef RT_SECTIONS
 #define RT_SECTIONS 0
 #endif
 // event counts of a sections build: [0] wave iterations, [1] lanes on a path, [2] vertex lanes,
 // [3] finishing lanes, [4] camera lanes, [5] MT loop wave iterations, [6] MT lanes tested,
-// [7] (lane, candidate) pairs, [8] 64-pair chunks if compacted, [9] finishing wave iterations with a
-// fold still draining, [10] lanes finishing with a fold still draining, [11] lanes draining at the top,
+// [7] (lane, candidate) pairs, [8] 64-pair chunks, [9] finishing wave iterations with a fold still
+// draining, [10] lanes finishing with a fold still draining, [11] lanes draining at the top,
 // [12] MT lanes on ray A, [13] ray A pairs, [14] MT hits (fp64 part passed), [15] scratch, [16..18]
 // distinct candidate triangles of the wave (ray A, ray B, either)
 #define RT_SEC_COUNTS 20
-#ifndef RT_PAD_VALU
-#define RT_PAD_VALU 0
-#endif
-// leaf boxes per group in the box loop: one scalar-load wait per 2 boxes (s_load_dwordx16) instead of
-// one per box; +0.9 % C4 over 1 (tools/ab_libs.py; 2: +0.6 %)
-#ifndef RT_BOX_UNROLL
-#define RT_BOX_UNROLL 4
-#endif
-// a path that ends while the previous fold still drains: its fold starts at the top of the next
-// iteration (1) instead of completing the previous fold at once after the iteration's stores (0);
-// A/B: 5926 -> 5650 Msamples/s (slower, as the early drain)
-#ifndef RT_DEFER_FOLD
-#define RT_DEFER_FOLD 0
-#endif
-// NARROW Moller-Trumbore loop: the next candidate's triangle read from LDS one test ahead (A/B knob)
-#ifndef RT_MT_PREFETCH
-#define RT_MT_PREFETCH 0
-#endif
-#if RT_MT_PREFETCH && RT_MT_FLOAT
-#error "RT_MT_PREFETCH is an A/B of the double-precision loop: build it with RT_MT_FLOAT=0"
-#endif
-// Moller-Trumbore spread over the wave through an LDS (lane, candidate) pair list (A/B build; the host
-// sizes the list from RT_PAIR_CAP).  C4: 6209 -> 5294 Msamples/s (MT loop iterations 13.5 -> 5.6 per
-// trace step at 91 % lane use, but each chunk costs the list writes, 10 ds_bpermute and the hit
-// returns, and ray B loses its early exit)
-#ifndef RT_MT_COMPACT
-#define RT_MT_COMPACT 0
-#endif
-// fold levels drained per iteration at the top of the loop, their ring loads issued together: a fold
-// then rarely still drains when the next path ends (where completing it waits on loads issued after
-// the iteration's stores).  C4 1024 spp: 1 level 5935, 2 6117, 3 6198, 4 6195 Msamples/s
-// (tools/ab_libs.py, profiles/r02/ab/ab_drain_depth.json)
-#ifndef RT_DRAIN_STEP
-#define RT_DRAIN_STEP 3
-#endif
-// ring levels loaded together when a fold is completed at once (drain_all; A/B knob)
-#ifndef RT_DRAIN_BATCH
-#define RT_DRAIN_BATCH 2
-#endif
-// fold ring layout: 1 = lane-major ([thread][position]: a lane's consecutive levels share cache
-// lines, so a drain read follows its push in L2), 0 = position-major ([position][thread]) (A/B knob)
-#ifndef RT_RING_LANE_MAJOR
-#define RT_RING_LANE_MAJOR 1
-#endif
-#if RT_RING_LANE_MAJOR
-#define RING_AT(p) ((size_t)gtid * Q.stack_depth + (p))
-#else
-#define RING_AT(p) ((size_t)(p) * Q.total_threads + gtid)
-#endif
-// complete the previous fold at the top of the iteration when the path will end in it (A/B knob:
-// -1.8 % C4, -2.5 % C5)
-#ifndef RT_EARLY_DRAIN
-#define RT_EARLY_DRAIN 0
-#endif
 
-// the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
-#ifndef RT_COH_BVH_MIN_WAVES
-#define RT_COH_BVH_MIN_WAVES 8
-#endif
+// Tuned constants (A/B history: DESIGN.md 6.4, profiles/r02/ab/):
+//  * work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
+//    more than one item per lane, so the launch tail stays one item long);
+//  * leaf boxes per scalar-load group in the box loop (one wait per 4 boxes; +0.9 % C4 over 1);
+//  * fold levels drained per iteration at the top of the loop, their ring loads issued together (a fold
+//    then rarely still drains when the next path ends): C4 1 level 5935, 2 6117, 3 6198, 4 6195 Msamples/s;
+//  * ring levels loaded together when a fold is completed at once (drain_all).
+constexpr uint32_t WQ_BATCH = 64u;
+constexpr int BOX_UNROLL = 4;
+constexpr uint32_t DRAIN_STEP = 3;
+constexpr uint32_t DRAIN_BATCH = 2;
+// fold ring layout: lane-major ([thread][position]): a lane's consecutive levels share cache lines, so a
+// drain read follows its push in L2
+#define RING_AT(p) ((size_t)gtid * Q.stack_depth + (p))
 
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
@@ -295,7 +205,6 @@ template <bool EXACT, bool BVH, bool NARROW>
 __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
-    constexpr uint32_t TQ = BVH ? 4u : (uint32_t)RT_LDS_TRI_QUADS;   // float4s per triangle in S.tris
     SceneView S;
     S.n_nodes = P.n_nodes;
     if (BVH) {
@@ -314,23 +223,20 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             S.mats = dm; S.lnodes = dl; S.ltris = dlt;
         }
     } else {
-        // stage the scene into LDS once per workgroup (nodes | tris | mats | lnodes | ltris; the leaf boxes
-        // are read with scalar loads)
-        // (tris | mats | lnodes | ltris; the BVH nodes stay in HBM -- only a ray with a non-finite
-        // reciprocal direction walks them -- and the leaf boxes are read with scalar loads)
-        // (triangles at a stride of TQ float4s: rt_kernels.h RT_LDS_TRI_QUADS)
+        // stage the scene into LDS once per workgroup: tris | mats | lnodes | ltris (the BVH nodes stay in
+        // HBM -- only a ray with a non-finite reciprocal direction walks them -- and the leaf boxes are read
+        // with scalar loads)
         const uint32_t tq = 4 * P.n_tris, mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
         float4* dt = lds_scene;
-        float4* dm = dt + TQ * P.n_tris;
+        float4* dm = dt + tq;
         float4* dl = dm + mq;
         float4* dlt = dl + lq;
-        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[(i >> 2) * TQ + (i & 3u)] = P.tris[i];
+        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[i] = P.tris[i];
         for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
         for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
         for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
         __syncthreads();
         S.nodes = P.nodes; S.tris = dt; S.mats = dm; S.lnodes = dl; S.ltris = dlt; S.lboxes = nullptr;
-        S.tq = TQ;
     }
 
     const uint32_t lane = __lane_id();
@@ -342,15 +248,12 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     auto lsu = [&](uint32_t f) -> uint32_t& { return reinterpret_cast<uint32_t*>(lstate)[f * 256u + tib]; };
     auto ls3 = [&](uint32_t f) { return V3{lsf(f), lsf(f + 1), lsf(f + 2)}; };
     auto st3 = [&](uint32_t f, V3 v) { lsf(f) = v.x; lsf(f + 1) = v.y; lsf(f + 2) = v.z; };
-    // leaf-box variant: the wave's (lane, candidate) pair list after the lane state (P.pair_cap entries)
-    uint16_t* const plist = reinterpret_cast<uint16_t*>(lstate + (P.has_light ? (EXACT ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256u) +
-                            (threadIdx.x >> 6) * P.pair_cap;
     const float PDF = 1.0f / (2.0f * PI_F);   // WhittedMaterial::PDF_at_the_sample, MC/WhittedMaterial.h:44-56
     // the leaf-box variant divides with rt_device.h div_fast (y = the divisor's correctly rounded
     // reciprocal; C4 +1.1 %); the BVH variant keeps the IEEE division sequence (its register budget: C5
-    // -2 % with div_fast)
-    auto sdiv = [](float x, float d, float y) { return (BVH && !RT_BVH_DIV_FAST) ? x / d : div_fast(x, d, y); };
-    auto vdiv = [](V3 a, float d, float y) { return (BVH && !RT_BVH_DIV_FAST) ? divs(a, d) : divs_fast(a, d, y); };
+    // -2.5 % with div_fast)
+    auto sdiv = [](float x, float d, float y) { return BVH ? x / d : div_fast(x, d, y); };
+    auto vdiv = [](V3 a, float d, float y) { return BVH ? divs(a, d) : divs_fast(a, d, y); };
     // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
     // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
     // pixel's samples in frame order (MC/Renderer.cpp:128-133).  The kernel issues no global load
@@ -362,103 +265,56 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         const size_t blk = Q.lbuf_pixel_major ? (size_t)local * ((Q.n_frames + 3u) >> 2) + (fidx >> 2)
                                               : (size_t)(fidx >> 2) * Q.lbuf_stride + local;
         const size_t at = (blk * 4u + (fidx & 3u)) * 3u;
-#if RT_PARK_NT
-        // write-once data: streaming stores, so parked lines do not evict the fold ring's lines from L2
-        __builtin_nontemporal_store(L.x, &Q.lbuf[at]);
-        __builtin_nontemporal_store(L.y, &Q.lbuf[at + 1]);
-        __builtin_nontemporal_store(L.z, &Q.lbuf[at + 2]);
-#else
         Q.lbuf[at] = L.x;
         Q.lbuf[at + 1] = L.y;
         Q.lbuf[at + 2] = L.z;
-#endif
     };
-    // one fold step of the draining path: L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
-    // (MC/Renderer.cpp:208,213), inner level first
-    auto drain_step = [&](uint32_t& dleft) {
+    // up to N fold steps of the draining path, L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
+    // (MC/Renderer.cpp:208,213), inner level first, from ring position `pos` down; the N ring loads are
+    // issued together (levels past the fold re-read the first one, unused).  Returns the levels folded.
+    auto fold_n = [&](auto NC, uint32_t& pos, uint32_t dleft, V3& L) -> uint32_t {
+        constexpr uint32_t N = decltype(NC)::value;
         CKParams& Q = kargs4();
-#if RT_DRAIN_STEP > 1
-        {   // up to RT_DRAIN_STEP levels per iteration, their ring loads issued together
-            const uint32_t R = Q.stack_depth;
-            uint32_t pos = lsu(VS_DPOS);
-            float4 e[RT_DRAIN_STEP];
-            int m[RT_DRAIN_STEP];
+        const uint32_t R = Q.stack_depth;
+        float4 e[N];
+        int m[N];
 #pragma unroll
-            for (uint32_t j = 0; j < RT_DRAIN_STEP; ++j) {
-                const uint32_t pj = pos >= j ? pos - j : pos + R - j;
-                const uint32_t at = j < dleft ? pj : pos;
-                ring_load(Q, RING_AT(at), e[j], m[j]);
-            }
-            V3 L = ls3(VS_DL);
-#pragma unroll
-            for (uint32_t j = 0; j < RT_DRAIN_STEP; ++j) {
-                if (j < dleft) {
-                    const float4 mb2 = S.mats[2 * m[j]];
-                    const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                    L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
-                }
-            }
-            const uint32_t n = dleft < RT_DRAIN_STEP ? dleft : RT_DRAIN_STEP;
-            dleft -= n;
-            if (dleft == 0u) {
-                complete(L, lsu(VS_DT0), lsu(VS_DT1));
-            } else {
-                st3(VS_DL, L);
-                lsu(VS_DPOS) = pos >= n ? pos - n : pos + R - n;
-            }
-            return;
+        for (uint32_t j = 0; j < N; ++j) {
+            const uint32_t pj = pos >= j ? pos - j : pos + R - j;
+            ring_load(Q, RING_AT(j < dleft ? pj : pos), e[j], m[j]);
         }
-#endif
-        const uint32_t pos = lsu(VS_DPOS);
-        float4 e;
-        int m;
-        ring_load(Q, RING_AT(pos), e, m);
-        const float4 mb2 = S.mats[2 * m];
-        const V3 f = (e.w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-        const V3 L = add(V3{e.x, e.y, e.z}, vdiv(vdiv(muls(mul(ls3(VS_DL), f), e.w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
-        dleft = dleft - 1u;
+#pragma unroll
+        for (uint32_t j = 0; j < N; ++j) {
+            if (j < dleft) {
+                const float4 mb2 = S.mats[2 * m[j]];
+                const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
+                L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
+            }
+        }
+        const uint32_t n = dleft < N ? dleft : N;
+        pos = pos >= n ? pos - n : pos + R - n;
+        return n;
+    };
+    // the top of an iteration: DRAIN_STEP levels of the draining fold
+    auto drain_step = [&](uint32_t& dleft) {
+        uint32_t pos = lsu(VS_DPOS);
+        V3 L = ls3(VS_DL);
+        dleft -= fold_n(std::integral_constant<uint32_t, DRAIN_STEP>{}, pos, dleft, L);
         if (dleft == 0u) {
             complete(L, lsu(VS_DT0), lsu(VS_DT1));
         } else {
             st3(VS_DL, L);
-            lsu(VS_DPOS) = (pos == 0u ? Q.stack_depth : pos) - 1u;
+            lsu(VS_DPOS) = pos;
         }
     };
-    // the rest of a draining fold at once (a path ended while the previous one still drains): the ring
-    // loads of RT_DRAIN_BATCH levels are issued together, then folded in order, so the wave waits for
-    // one load latency per batch instead of one per level
+    // the rest of a draining fold at once (a path ended while the previous one still drains): the wave
+    // waits for one load latency per DRAIN_BATCH levels instead of one per level
     auto drain_all = [&](uint32_t& dleft) {
-#if RT_DRAIN_BATCH > 1
         if (dleft == 0u) return;
-        CKParams& Q = kargs4();
-        const uint32_t R = Q.stack_depth;
         uint32_t pos = lsu(VS_DPOS);
         V3 L = ls3(VS_DL);
-        while (dleft != 0u) {
-            float4 e[RT_DRAIN_BATCH];
-            int m[RT_DRAIN_BATCH];
-#pragma unroll
-            for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
-                const uint32_t pj = pos >= j ? pos - j : pos + R - j;
-                const uint32_t at = j < dleft ? pj : pos;   // levels past the fold re-read the first one (unused)
-                ring_load(Q, RING_AT(at), e[j], m[j]);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < RT_DRAIN_BATCH; ++j) {
-                if (j < dleft) {
-                    const float4 mb2 = S.mats[2 * m[j]];
-                    const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                    L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
-                }
-            }
-            const uint32_t n = dleft < RT_DRAIN_BATCH ? dleft : RT_DRAIN_BATCH;
-            pos = pos >= n ? pos - n : pos + R - n;
-            dleft -= n;
-        }
+        while (dleft != 0u) dleft -= fold_n(std::integral_constant<uint32_t, DRAIN_BATCH>{}, pos, dleft, L);
         complete(L, lsu(VS_DT0), lsu(VS_DT1));
-#else
-        while (dleft != 0u) drain_step(dleft);
-#endif
     };
 
     bool alive = true, have_pixel = false, in_path = false;
@@ -486,23 +342,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
     uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     if (EXACT) lsu(VS_BASE) = 0u;
-#if RT_DEFER_FOLD
-    // a finished path's fold recorded for the top of the next iteration (the previous fold still drained)
-    bool deferred = false;
-    auto start_deferred = [&]() {
-        CKParams& Q = kargs4();
-        drain_all(dleft);   // the previous fold completes first
-        const uint32_t R = Q.stack_depth;
-        const uint32_t m = lsu(VS_PCOS);
-        const uint32_t nb = lsu(VS_BASE);
-        st3(VS_DL, ls3(VS_LD));
-        lsu(VS_DPOS) = (nb == 0u ? R : nb) - 1u;   // the innermost level, just below the next path's base
-        lsu(VS_DT0) = lsu(VS_LOCAL);
-        lsu(VS_DT1) = lsu(VS_FRAME) - 1u - Q.first_frame;
-        dleft = m;
-        deferred = false;
-    };
-#endif
     // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
     const uint32_t NN = S.n_nodes;
     uint32_t tiA = NN, tiB = NN;
@@ -528,7 +367,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
     // Lanes without a work item take the next ones from the wave's pool, in lane order.  With `refill`
     // (the top of the iteration, before any store) an empty pool is refilled from the device counter;
-    // without it (RT_LATE_ITEMS: after the path-end block, so a lane whose item just ended starts the
+    // without it (after the path-end block, so a lane whose item just ended starts the
     // next one's camera ray in the same iteration) only the pool's items are handed out -- no atomic,
     // so nothing waits for the iteration's stores.
     auto take_items = [&](const bool refill) {
@@ -579,39 +418,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     };
     for (;;) {
         SEC_MARK(0);
-#if RT_PAD_VALU
-        {   // diagnostic: RT_PAD_VALU independent VALU ops per iteration (VALU-throughput sensitivity)
-            float a0 = (float)lane, a1 = a0 + 1.0f, a2 = a0 + 2.0f, a3 = a0 + 3.0f;
-#pragma unroll
-            for (int i = 0; i < RT_PAD_VALU / 4; ++i) {
-                asm volatile("v_add_f32 %0, 1.0, %0\n v_add_f32 %1, 1.0, %1\n v_add_f32 %2, 1.0, %2\n v_add_f32 %3, 1.0, %3"
-                             : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3));
-            }
-            asm volatile("" : : "v"(a0), "v"(a1), "v"(a2), "v"(a3));
-        }
-#endif
-#if RT_DEFER_FOLD
-        if (EXACT && __any(deferred)) {
-            if (deferred) start_deferred();
-        } else
-#endif
         if (EXACT && __any(dleft != 0u)) {
             if (dleft != 0u) {
-#if RT_EARLY_DRAIN
-                // a lane whose path ends in this iteration's service (the same decision) completes its
-                // previous fold here, before the iteration's stores: its ring loads then wait for no
-                // store of this iteration (vmcnt counts both)
-                bool ends = false;
-                if (in_path && (!BVH || (tiA >= NN && tiB >= NN))) {
-                    bool em = false;
-                    if (triA >= 0) em = S.mats[2 * f2i(S.tris[TQ * triA].w)].w != 0.0f;
-                    ends = triA < 0 || em || (pend && !cont);
-                }
-                if (ends) drain_all(dleft);
-                else drain_step(dleft);
-#else
                 drain_step(dleft);
-#endif
             }
         }
         SEC_MARK(3);
@@ -636,9 +445,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             bool emissive = false;
             if (hasA && triA >= 0) {
                 // BVH variant: the material came with the hit (tri_mat)
-                mat = (BVH && RT_HIT_MAT == 1) ? (triA >> 24)
-                    : (BVH && RT_HIT_MAT == 2) ? (int)lsu(P.has_light ? VS_HMAT_LIT : VS_HMAT_UNLIT)
-                                               : f2i(S.tris[TQ * (BVH ? (triA & 0xFFFFFF) : triA)].w);
+                mat = f2i(S.tris[4 * triA].w);
                 emissive = S.mats[2 * mat].w != 0.0f;
             }
             bool vertex = false;
@@ -723,8 +530,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
             if (vertex) {
                 // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
-                const int ti3 = (BVH && RT_HIT_MAT == 1) ? (triA & 0xFFFFFF) : triA;
-                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[TQ * ti3 + 3];
+                const int ti3 = triA;
+                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[4 * ti3 + 3];
                 const V3 wo = neg(dA);
                 const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
                 const V3 N{tq3.x, tq3.y, tq3.z};
@@ -745,18 +552,18 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const float4 mb = S.mats[2 * mat];
                         const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                         const V3 ldu = vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
-                                                 (BVH && !RT_BVH_DIV_FAST) ? 0.0f : rcp_f32(sd2)),
+                                                 BVH ? 0.0f : rcp_f32(sd2)),
                                             Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
                         st3(VS_LD, ldu);
                         dB = wl;
                         // a zero unoccluded term (the light behind the surface: f = 0) makes the verdict pick
                         // between +0 and +-0, which no accumulation can tell apart (sums start at +0): no
                         // shadow ray then (the direct term is taken as +0, as for an occluded light)
-                        hasB = !(RT_ZERO_LD_SKIP && ldu.x == 0.0f && ldu.y == 0.0f && ldu.z == 0.0f);
+                        hasB = !(ldu.x == 0.0f && ldu.y == 0.0f && ldu.z == 0.0f);
                         // triangles (near-)coplanar with the sampled light triangle are hit, if at all, within
                         // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
                         // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
-                        if (NARROW && !BVH && RT_LIGHT_SKIP) bskip = sc2 >= 0.25f ? lskip : 0u;
+                        if (NARROW && !BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
                     }
                     // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
                     cont = G.next() < Q.rr && depth < 4096u;
@@ -804,23 +611,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
                     const uint32_t m = (uint32_t)(fold_top + 1);
                     const uint32_t base = lsu(VS_BASE);
-#if RT_DEFER_FOLD
-                    // every sample has its own parked slot, so folds may complete in any order: a sample
-                    // without levels completes at once, and a fold that would wait for the previous one
-                    // is only recorded here (L in VS_LD, its level count in VS_PCOS; both are free until
-                    // the next path's first vertex) and started at the top of the next iteration, whose
-                    // loads follow no store of that iteration
-                    if (m != 0u && dleft != 0u) {
-                        st3(VS_LD, L);
-                        lsu(VS_PCOS) = m;
-                        uint32_t nb = base + m;
-                        if (nb >= Q.stack_depth) nb -= Q.stack_depth;
-                        lsu(VS_BASE) = nb;
-                        deferred = true;
-                    } else
-#else
                     drain_all(dleft);   // the previous sample's fold completes first
-#endif
                     if (m == 0u) {
                         complete(L, local, fidx);
                     } else {
@@ -842,9 +633,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
         }
 
-#if RT_LATE_ITEMS
         take_items(false);
-#endif
         SEC_MARK(4);
         // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
         if (have_pixel && !in_path) {
@@ -861,7 +650,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             cy = cy * 2.0f - 1.0f;
             float tg[4];
             mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], (BVH && !RT_BVH_DIV_FAST) ? 0.0f : rcp_f32(tg[3])));
+            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
             float wd[4];
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
@@ -878,9 +667,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         }
 
         if (!__any(have_pixel || alive)) {
-#if RT_DEFER_FOLD
-            if (EXACT && deferred) start_deferred();
-#endif
             if (EXACT) drain_all(dleft);
             break;
         }
@@ -898,11 +684,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // ======================= trace both rays of every lane =======================
         if (!BVH) {
         const bool trA = in_path && hasA, trB = in_path && hasB;
-#if RT_MT_FLOAT
-        triA = -1; occB = false;   // tA is formed after the Moller-Trumbore loop
-#else
         tA = 1.7976931348623157e308; triA = -1; occB = false;
-#endif
         // the reciprocal directions are computed here, not when the rays are set up: they are then
         // temporaries of the box loop instead of 6 registers live across the iteration
         rA = rcp3(dA); rB = rcp3(dB);
@@ -912,9 +694,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // (A first) without selecting between two
         uint64_t ca = 0, cb = 0;
         uint32_t ma = 0, mb = 0;
-        for (int rep = 0; rep < RT_REP_BOX; ++rep) {   // RT_REP_BOX > 1: cost-attribution builds only
-            if (RT_REP_BOX > 1) { ca = cb = 0; ma = mb = 0; asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z)); }
-            // a box is one 32-byte scalar load (s_load_dwordx8; a group of RT_BOX_UNROLL boxes waits once)
+        {
+            // a box is one 32-byte scalar load (s_load_dwordx8; a group of BOX_UNROLL boxes waits once)
             cbox8* bx = (cbox8*)kargs4().lboxes;
             const uint32_t nb = kargs4().n_lboxes;
             auto one_box = [&](const box8 q) {   // (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, mask 0-31, mask 32-63), rt_layout.h
@@ -934,19 +715,16 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 }
             };
             uint32_t b = 0;
-#if RT_BOX_UNROLL > 1
-            for (; b + RT_BOX_UNROLL <= nb; b += RT_BOX_UNROLL) {
-                box8 q[RT_BOX_UNROLL];
+            for (; b + BOX_UNROLL <= nb; b += BOX_UNROLL) {
+                box8 q[BOX_UNROLL];
 #pragma unroll
-                for (int u = 0; u < RT_BOX_UNROLL; ++u) q[u] = bx[b + u];
+                for (int u = 0; u < BOX_UNROLL; ++u) q[u] = bx[b + u];
 #pragma unroll
-                for (int u = 0; u < RT_BOX_UNROLL; ++u) one_box(q[u]);
+                for (int u = 0; u < BOX_UNROLL; ++u) one_box(q[u]);
             }
-#endif
             for (; b < nb; ++b) one_box(bx[b]);
-            if (RT_REP_BOX > 1) asm volatile("" : : "v"(ca), "v"(cb), "v"(ma), "v"(mb));
         }
-        if (NARROW) { ca = ma; cb = RT_LIGHT_SKIP ? (mb & ~bskip) : mb; }
+        if (NARROW) { ca = ma; cb = mb & ~bskip; }
         if (!trA || !fin) ca = 0;
         if (!trB || !fin) cb = 0;
         if (!fin && (trA || trB)) {
@@ -1014,217 +792,45 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
         // Moller-Trumbore on the candidates in DFS order: ray A first (closest hit, the later leaf wins
         // ties), then ray B (stops at the first blocking hit)
-        auto mt_loop = [&](uint64_t ca, uint64_t cb, double& tA, int& triA, bool& occB) {
-#if RT_MT_FLOAT
-            // Moller-Trumbore decided in float where the float values decide it (rt_device.h mt_float);
-            // the closest hit is kept as its triangle and q = tn * rcp(den) (relative error < 2^-22), which
-            // orders the hits; its t = (double)tn * rcp_f64_of_f32(den) is formed once, after the loop, from
-            // the float part recomputed for that triangle (the same operations: the same tn, den)
-            float tnA = 0.0f, denA = 1.0f;
-            auto t_of = [](float tn, float den) { return (double)tn * rcp_f64_of_f32(den); };
-            auto test = [&](const bool useA, const int tri, uint64_t& rest) {
-                const V3 d = useA ? dA : dB;
-                float4 t0, t1, t2;
-                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
-                float tn, den, b2n, b3n;
-                const int c = mt_float(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, tn, den, b2n, b3n);
+        auto test = [&](const bool useA, const int tri, uint64_t& rest) {
+            const V3 d = useA ? dA : dB;
+            const float4* T = S.tris + 4 * tri;
+            const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+            double t;
+            const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
 #if RT_SECTIONS
-                SEC_COUNT(5, 1u);
-                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
-                SEC_COUNT(12, (uint32_t)__popcll(__ballot(useA)));
-                SEC_COUNT(14, (uint32_t)__popcll(__ballot(c != MT_MISS)));
-                SEC_COUNT(19, (uint32_t)__popcll(__ballot(c == MT_OPEN)));
+            SEC_COUNT(5, 1u);
+            SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
+            SEC_COUNT(12, (uint32_t)__popcll(__ballot(useA)));
+            SEC_COUNT(14, (uint32_t)__popcll(__ballot(mh)));
 #endif
-                if (c == MT_MISS) return;
-                double t = 0.0;
-                float q;
-                if (c == MT_OPEN) {   // rare: the barycentric boundary within 1e-5, or badly scaled operands
-                    if (!mt_open(tn, den, b2n, b3n, t)) return;
-                    q = (float)t;
-                } else {
-                    q = tn * __builtin_amdgcn_rcpf(den);   // v_rcp_f32: 1 ulp; den, tn in [2^-40, 2^40]
-                }
+            if (mh) {
                 if (useA) {
-                    // the reference's `t <= tA` (MC/BVH.h:97-100: the later leaf wins a tie), decided by q
-                    // outside a 2^-19 band around qA (q, qA within 2^-22 of t, tA when both are normal
-                    // -- an MT_OPEN hit or best is compared exactly)
-                    const float qA = tnA * __builtin_amdgcn_rcpf(denA);
-                    bool take;
-                    if (triA < 0) take = true;
-                    else if (c == MT_HIT && q < qA * (1.0f - 0x1p-19f)) take = true;
-                    else if (c == MT_HIT && q > qA * (1.0f + 0x1p-19f)) take = false;
-                    else take = (c == MT_OPEN ? t : t_of(tn, den)) <= t_of(tnA, denA);
-                    if (take) { tnA = tn; denA = den; triA = tri; }
-                } else {
-                    // blocking: !(slen < t + 0.01f) (MC/Renderer.cpp:184), decided by q + 0.01f outside a
-                    // 2^-18 band around slen
-                    const float s = q + 0.01f;
-                    bool blk;
-                    if (c == MT_HIT && s > slen * (1.0f + 0x1p-18f)) blk = false;
-                    else if (c == MT_HIT && s < slen * (1.0f - 0x1p-18f)) blk = true;
-                    else blk = !((double)slen < (c == MT_OPEN ? t : t_of(tn, den)) + (double)0.01f);
-                    if (blk) {
-                        occB = true;
-                        rest = 0;   // B's candidates come last: nothing else to test
-                    }
-                }
-            };
-            // (a lane that walked the BVH -- non-finite reciprocal -- has its walk's tA)
-            auto finish_mt = [&]() { if (fin) tA = t_of(tnA, denA); };
-#else
-            auto finish_mt = [&]() {};
-            auto test = [&](const bool useA, const int tri, uint64_t& rest) {
-                const V3 d = useA ? dA : dB;
-                float4 t0, t1, t2;
-                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
-                double t;
-                const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
-#if RT_SECTIONS
-                SEC_COUNT(5, 1u);
-                SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
-                SEC_COUNT(12, (uint32_t)__popcll(__ballot(useA)));
-                SEC_COUNT(14, (uint32_t)__popcll(__ballot(mh)));
-#endif
-                if (mh) {
-                    if (useA) {
-                        if (t <= tA) { tA = t; triA = tri; }
-                    } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                        occB = true;
-                        rest = 0;   // B's candidates come last: nothing else to test
-                    }
-                }
-            };
-#endif
-            if (NARROW && RT_MT_PREFETCH) {
-                // the next candidate's triangle is read from LDS before the current one is tested
-                uint64_t cm = ca | (cb << 32);
-                if (cm != 0) {
-                    uint32_t bit = (uint32_t)__builtin_ctzll(cm);
-                    cm &= cm - 1;
-                    const float4* T = S.tris + TQ * (bit & 31u);
-                    float4 u0 = T[0], u1 = T[1], u2 = T[2];
-                    for (;;) {
-                        const uint32_t nbit = cm != 0 ? (uint32_t)__builtin_ctzll(cm) : bit;
-                        const float4* N = S.tris + TQ * (nbit & 31u);
-                        const float4 n0 = N[0], n1 = N[1], n2 = N[2];
-                        const bool useA = bit < 32u;
-                        double t;
-                        const bool mh = moller_trumbore_od(V3{u0.x, u0.y, u0.z}, V3{u1.x, u1.y, u1.z}, V3{u2.x, u2.y, u2.z}, o, useA ? dA : dB, t);
-                        if (mh) {
-                            if (useA) {
-                                if (t <= tA) { tA = t; triA = (int)(bit & 31u); }
-                            } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
-                                occB = true;
-                                cm = 0;
-                            }
-                        }
-                        if (cm == 0) break;
-                        cm &= cm - 1;
-                        bit = nbit; u0 = n0; u1 = n1; u2 = n2;
-                    }
-                }
-            } else if (NARROW) {
-                uint64_t cm = ca | (cb << 32);
-                while (cm != 0) {
-                    const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
-                    cm &= cm - 1;
-                    test(bit < 32u, (int)(bit & 31u), cm);
-                }
-            } else {
-                while ((ca | cb) != 0) {
-                    const bool useA = ca != 0;
-                    const uint64_t cur = useA ? ca : cb;
-                    const int tri = __builtin_ctzll(cur);
-                    if (useA) ca = cur & (cur - 1);
-                    else cb = cur & (cur - 1);
-                    test(useA, tri, cb);
+                    if (t <= tA) { tA = t; triA = tri; }
+                } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                    occB = true;
+                    rest = 0;   // B's candidates come last: nothing else to test
                 }
             }
-            finish_mt();
         };
-        for (int rep = 1; rep < RT_REP_MT; ++rep) {   // cost-attribution builds only: results discarded
-            uint64_t xa = ca, xb = cb;
-            double xt = tA; int xtri = triA; bool xo = occB;
-            asm volatile("" : "+v"(xa), "+v"(xb), "+v"(o.x));
-            mt_loop(xa, xb, xt, xtri, xo);
-            asm volatile("" : : "v"(xt), "v"(xtri), "v"(xo));
-        }
-        if (RT_MT_COMPACT && kargs4().pair_cap != 0u) {
-            // Moller-Trumbore spread over the wave (A/B build RT_MT_COMPACT=1 + RT_PAIR_CAP; slower than the per-lane loop:
-            // DESIGN.md 6.1).  The lanes' (lane, candidate) pairs -- ray A's candidates, then ray B's, in
-            // DFS order -- are listed in LDS at the lane's exclusive prefix sum of pair counts; each
-            // 64-pair chunk runs one test per lane on the owner's ray (fetched with ds_bpermute), and the
-            // results return to their owners: a blocking ray-B hit by ballot over the owner's positions,
-            // ray-A hits in position (= DFS) order with the reference's `t <= tA` update
-            // (MC/BVH.h:97-100), so the closest hit and its tie rule are unchanged.
-            CKParams& Q = kargs4();
-            const uint32_t cap = Q.pair_cap;
-            const uint32_t nA = (uint32_t)__popcll(ca), n = nA + (uint32_t)__popcll(cb);
-            const uint32_t excl = wave_incl_scan(n) - n;
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + n), 63);
-            for (uint32_t w0 = 0; w0 < total; w0 += cap) {
-                const uint32_t wn = total - w0 < cap ? total - w0 : cap;
-                if (excl < w0 + wn && excl + n > w0) {
-                    // this lane's pairs inside the window: entry = owner lane | triangle << 6 | ray B << 12
-                    uint64_t a = ca, b = cb;
-                    uint32_t idx = excl;
-                    while ((a | b) != 0u && idx < w0 + wn) {
-                        const bool isA = a != 0u;
-                        const uint64_t cur = isA ? a : b;
-                        const uint32_t tri = (uint32_t)__builtin_ctzll(cur);
-                        if (isA) a = cur & (cur - 1u);
-                        else b = cur & (cur - 1u);
-                        if (idx >= w0) plist[idx - w0] = (uint16_t)(lane | (tri << 6) | (isA ? 0u : 4096u));
-                        ++idx;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                for (uint32_t c0 = 0; c0 < wn; c0 += 64u) {
-                    const uint32_t q = c0 + lane;
-                    const bool valid = q < wn;
-                    const uint32_t e = valid ? (uint32_t)plist[q] : 0u;
-                    const uint32_t own = e & 63u, tri = (e >> 6) & 63u;
-                    const bool isB = (e & 4096u) != 0u;
-                    // the owner's direction (A or B) and origin; both directions are fetched (every lane
-                    // takes part in a ds_bpermute) and selected per component
-                    V3 pd;
-                    pd.x = lane_f(own, dA.x); { const float v = lane_f(own, dB.x); pd.x = isB ? v : pd.x; }
-                    pd.y = lane_f(own, dA.y); { const float v = lane_f(own, dB.y); pd.y = isB ? v : pd.y; }
-                    pd.z = lane_f(own, dA.z); { const float v = lane_f(own, dB.z); pd.z = isB ? v : pd.z; }
-                    const V3 po{lane_f(own, o.x), lane_f(own, o.y), lane_f(own, o.z)};
-                    const float psl = lane_f(own, slen);
-                    double t = 0.0;
-                    bool hit = false;
-                    if (valid) {
-                        float4 t0, t1, t2;
-                tri_ld3(S.tris + TQ * tri, t0, t1, t2);
-                        hit = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, po, pd, t);
-                    }
-                    // this lane's pairs in the chunk: positions [s, s + n)
-                    const int s0 = (int)excl - (int)(w0 + c0);
-                    const int lo = s0 < 0 ? 0 : (s0 > 64 ? 64 : s0);
-                    const int hiA = s0 + (int)nA < 0 ? 0 : (s0 + (int)nA > 64 ? 64 : s0 + (int)nA);
-                    const int hi = s0 + (int)n < 0 ? 0 : (s0 + (int)n > 64 ? 64 : s0 + (int)n);
-                    // ray B: any blocking hit occludes (MC/Renderer.cpp:184)
-                    const uint64_t blk = __ballot(hit && isB && !((double)psl < t + (double)0.01f));
-                    if ((blk & bit_range(lo, hi)) != 0u) occB = true;
-                    // ray A: hits in position order, t <= tA (the later leaf wins a tie)
-                    uint64_t mine = __ballot(hit && !isB) & bit_range(lo, hiA);
-                    while (__any(mine != 0u)) {
-                        const uint32_t src = mine != 0u ? (uint32_t)__builtin_ctzll(mine) : lane;
-                        const uint32_t tlo = lane_u(src, (uint32_t)__double2loint(t)), thi = lane_u(src, (uint32_t)__double2hiint(t));
-                        const uint32_t htri = lane_u(src, tri);
-                        if (mine != 0u) {
-                            const double ht = __hiloint2double((int)thi, (int)tlo);
-                            if (ht <= tA) { tA = ht; triA = (int)htri; }
-                            mine &= mine - 1u;
-                        }
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (NARROW) {
+            // (a cap on the tests per lane and iteration, the rest carried to the next iteration, measured
+            // C4 -1 % at caps 6-10 and -10 % at 4: the carried state costs spills, profiles/r03/ab/)
+            uint64_t cm = ca | (cb << 32);
+            while (cm != 0) {
+                const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
+                cm &= cm - 1;
+                test(bit < 32u, (int)(bit & 31u), cm);
             }
         } else {
-            mt_loop(ca, cb, tA, triA, occB);
+            while ((ca | cb) != 0) {
+                const bool useA = ca != 0;
+                const uint64_t cur = useA ? ca : cb;
+                const int tri = __builtin_ctzll(cur);
+                if (useA) ca = cur & (cur - 1);
+                else cb = cur & (cur - 1);
+                test(useA, tri, cb);
+            }
         }
 #if RT_SECTIONS >= 3
         {   // [320 + tri] ray A's closest hits by triangle, [352] blocked ray-B lanes (fin lanes)
@@ -1300,11 +906,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         const int pk = slot == 0 ? parked0 : parked1;
                         if (pk < 0 || (!curA && occB)) continue;
                         V3 va, e1, e2;
-                        int pmat;   // the triangle's material, kept with the hit (the service reads no triangle)
                         if (qround) {
                             const float4* ta = kargs4().tabc + 3 * pk;
                             const float4 t0 = ta[0], t1 = ta[1], t2 = ta[2];
-                            pmat = f2i(t0.w);
                             // the exact leaf box: Triangle::Get3DAABB (MC/TriangleMesh.h:96-99)
                             if (!slab_hit_finite(r, __builtin_fminf(__builtin_fminf(t0.x, t1.x), t2.x), __builtin_fminf(__builtin_fminf(t0.y, t1.y), t2.y),
                                                  __builtin_fminf(__builtin_fminf(t0.z, t1.z), t2.z), __builtin_fmaxf(__builtin_fmaxf(t0.x, t1.x), t2.x),
@@ -1314,19 +918,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                             e1 = sub(V3{t1.x, t1.y, t1.z}, va);
                             e2 = sub(V3{t2.x, t2.y, t2.z}, va);
                         } else {
-                            const float4 t0 = S.tris[TQ * pk], t1 = S.tris[TQ * pk + 1], t2 = S.tris[TQ * pk + 2];
+                            const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
                             va = V3{t0.x, t0.y, t0.z}; e1 = V3{t1.x, t1.y, t1.z}; e2 = V3{t2.x, t2.y, t2.z};
-                            pmat = f2i(t0.w);
                         }
                         double t;
                         if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {
-                                // the later leaf wins ties; the index in bits 0-23, the material above
-                                if (t <= tA) {
-                                    tA = t;
-                                    triA = pk | (RT_HIT_MAT == 1 ? (pmat << 24) : 0);
-                                    if (RT_HIT_MAT == 2) lsu(kargs4().has_light ? VS_HMAT_LIT : VS_HMAT_UNLIT) = (uint32_t)pmat;
-                                }
+                                if (t <= tA) { tA = t; triA = pk; }   // the later leaf wins ties
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 ti = NN;
@@ -1401,7 +999,6 @@ hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* m
 
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh)
 {
-    if (bvh && RT_HIT_MAT == 2) return (size_t)((lit ? VS_HMAT_LIT : VS_HMAT_UNLIT) + 1) * 256 * sizeof(float);
     return (size_t)(lit ? (exact ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
 }
 

@@ -208,69 +208,9 @@ __device__ __forceinline__ bool moller_trumbore_od(const V3& a, const V3& e1, co
     const double b3 = (double)b3n * inv;
     return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
 }
-// The same test with the double arithmetic taken only where the float values cannot decide it.
-// Returns MT_MISS, MT_HIT (the reference's test passes; its t = (double)tn * rcp_f64_of_f32(den) and
-// q = tn * rcp(den) is within 2^-22 of it) or MT_OPEN (mt_open decides, as moller_trumbore_od).  With
-// tn, b2n, b3n of one strict sign s and 2^-40 <= |den|, |tn| <= 2^40:
-//   * sign(den) != s: inv = RN(1/den) is finite, nonzero and of den's sign, so t = tn * inv < 0: a miss;
-//   * |b2n| + |b3n| < |den| * 0.99999f (float, rounded): b2 + b3 < 1 - 9.9e-6 in double (each of the
-//     products b2n * inv, b3n * inv is rounded once, and inv once), so t > 0 and (1 - b2) - b3 > 0: a hit.
-// Everything else (the barycentric boundary within 1e-5, badly scaled operands) goes to mt_open.
-enum : int { MT_MISS = 0, MT_HIT = 1, MT_OPEN = 2 };
-__device__ __forceinline__ int mt_float(const V3& a, const V3& e1, const V3& e2, const V3& o, const V3& d, float& tn_o, float& den_o,
-                                        float& b2n_o, float& b3n_o)
-{
-    const V3 S = sub(o, a);
-    const V3 S1 = cross(d, e2), S2 = cross(S, e1);
-    const float den = dot(S1, e1);
-    const float tn = dot(S2, e2), b2n = dot(S1, S), b3n = dot(S2, d);
-    tn_o = tn; den_o = den; b2n_o = b2n; b3n_o = b3n;
-    const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
-    const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
-    if (!(pos || ngt)) return MT_MISS;
-    const float sb = __builtin_fabsf(b2n) + __builtin_fabsf(b3n), aden = __builtin_fabsf(den), atn = __builtin_fabsf(tn);
-    if (sb > aden * 1.00001f) return MT_MISS;
-    if (!(aden >= 0x1p-40f && aden <= 0x1p40f && atn >= 0x1p-40f && atn <= 0x1p40f)) return MT_OPEN;
-    if (pos != (den > 0.0f)) return MT_MISS;
-    return sb < aden * 0.99999f ? MT_HIT : MT_OPEN;
-}
-// the double part of moller_trumbore_od for an MT_OPEN case
-__device__ __forceinline__ bool mt_open(float tn, float den, float b2n, float b3n, double& t_out)
-{
-    const double inv = rcp_f64_of_f32(den);
-    const double t = (double)tn * inv;
-    t_out = t;
-    const double b2 = (double)b2n * inv;
-    const double b3 = (double)b3n * inv;
-    return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
-}
 __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const V3& e2, const Ray& r, double& t_out)
 {
     return moller_trumbore_od(a, e1, e2, r.o, r.d, t_out);
-}
-
-// ------------------------------------------------------------------------------ wave-level helpers
-// inclusive prefix sum over the 64 lanes of a wave (every lane active): row shifts 1, 2, 4, 8 within
-// each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals (GFX9 DPP)
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
-{
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
-    return v;
-}
-// the value of `v` in lane `src` (every lane active; ds_bpermute_b32)
-__device__ __forceinline__ float lane_f(uint32_t src, float v) { return __int_as_float(__builtin_amdgcn_ds_bpermute((int)(src << 2), __float_as_int(v))); }
-__device__ __forceinline__ uint32_t lane_u(uint32_t src, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
-// bits [lo, hi) of a 64-bit mask, 0 <= lo <= hi <= 64
-__device__ __forceinline__ uint64_t bit_range(int lo, int hi)
-{
-    const uint64_t h = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-    const uint64_t l = lo >= 64 ? ~0ull : ((1ull << lo) - 1ull);
-    return h & ~l;
 }
 
 // ------------------------------------------------------------------------------ packed f32

@@ -2,13 +2,6 @@
 #ifndef RT_KERNELS_H
 #define RT_KERNELS_H
 
-// float4s per triangle in the leaf-box vertex kernel's LDS copy of the triangles (A/B knob): 5 (one pad)
-// puts the triangles of a 16-lane ds_read_b128 group on 16 different bank phases (20 dwords apart, mod
-// 64) instead of 4 (16 dwords apart).  C4: 6861 (4) vs 6869 (5, ds_read_b96) vs 6839 (5, ds_read_b128)
-// Msamples/s -- the bank conflicts do not bind
-#ifndef RT_LDS_TRI_QUADS
-#define RT_LDS_TRI_QUADS 4
-#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -64,8 +57,6 @@ struct KParams {
     uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
     uint32_t lds_pad;               // diagnostic: unused dynamic LDS bytes per workgroup (occupancy experiments)
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
-    uint32_t pair_cap;              // vertex kernel, leaf-box variant: (lane, candidate) pairs per wave in the LDS pair
-                                    // list after the lane state -- Moller-Trumbore spread over the wave (0: per-lane loop)
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray

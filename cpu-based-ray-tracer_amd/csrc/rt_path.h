@@ -60,7 +60,6 @@ struct SceneView {
     const float4* ltris;
     uint32_t n_nodes;
     const float4* lboxes;   // small scenes: distinct leaf boxes (rt_layout.h), else unused
-    uint32_t tq = 4;        // float4s per triangle in `tris` (the leaf-box vertex kernel pads its LDS copy)
 };
 
 // One traversal: closest hit (shadow == false) or any blocking hit (shadow == true).
@@ -90,7 +89,7 @@ __device__ __forceinline__ void traverse_impl(const SceneView& S, const Ray& r, 
         }
         if (parked >= 0) {
             if (COUNT) ++tri_tests;
-            const float4 t0 = S.tris[S.tq * parked], t1 = S.tris[S.tq * parked + 1], t2 = S.tris[S.tq * parked + 2];
+            const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
             double t;
             if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
                 if (shadow) {

@@ -1,0 +1,318 @@
+"""tools/sim_candidates.py -- statistical model of the vertex kernel's Moller-Trumbore loop (C4 Cornell).
+
+Simulates waves of 64 lanes, each lane tracing paths of one pixel of an 8x8 tile frame after frame,
+one path vertex per iteration (the vertex kernel's schedule, rt_coherent.hip): ray A (camera or
+indirect) and ray B (shadow).  Geometry in float64 with numpy random numbers -- not the reference's
+bits, only its distributions.  Per wave-iteration it reports the length of the per-lane candidate
+loop (max over lanes) under several candidate-selection policies, to decide which one to build.
+
+    python tools/sim_candidates.py [--waves 2000] [--iters 40]
+"""
+import argparse
+import importlib.util
+import os
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load_rt():
+    spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(REPO, "cpu-based-ray-tracer_amd", "__init__.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--waves", type=int, default=2000)
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args()
+    rt = load_rt()
+    s = rt.Scene.cornell()
+    info = s.info()
+    nf, ni, tf, ti = s.export()
+    NT = info.n_tris
+    A = tf[:, 0:3].astype(np.float64); B = tf[:, 3:6].astype(np.float64); Cc = tf[:, 6:9].astype(np.float64)
+    NRM = tf[:, 9:12].astype(np.float64)
+    E1 = B - A; E2 = Cc - A
+    mesh = ti[:, 0]
+    light_mesh = info.light_mesh
+    albedo_zero = np.zeros(NT, bool)
+    emissive = mesh == light_mesh
+    ltris = np.nonzero(emissive)[0]
+    # leaf boxes: identical leaf boxes merged (rt_scene.cpp)
+    leaves = [k for k in range(ni.shape[0]) if ni[k, 2] >= 0]
+    boxes = {}
+    for k in leaves:
+        key = tuple(nf[k, :6].tolist())
+        boxes.setdefault(key, 0)
+        boxes[key] |= 1 << int(ni[k, 2])
+    bkeys = list(boxes.keys())
+    BLO = np.array([k[:3] for k in bkeys]); BHI = np.array([k[3:6] for k in bkeys])
+    BM = np.array([boxes[k] for k in bkeys], dtype=np.uint64)
+    NB = len(bkeys)
+    box_of_tri = np.zeros(NT, int)
+    for b in range(NB):
+        for t in range(NT):
+            if (int(BM[b]) >> t) & 1:
+                box_of_tri[t] = b
+    print(f"{NT} triangles, {NB} leaf boxes, light mesh {light_mesh}, light tris {ltris.tolist()}")
+    # light-plane skip mask (rt_scene.cpp): triangles within 0.0015 of a light triangle's plane, parallel
+    ln = NRM[ltris[0]] / np.linalg.norm(NRM[ltris[0]])
+    d0 = ln @ A[ltris[0]]
+    near = np.all(np.abs(np.stack([A @ ln, B @ ln, Cc @ ln], 1) - d0) <= 0.0015, axis=1)
+    par = np.abs(NRM @ ln) >= 0.999
+    skipmask = np.uint64(sum(1 << t for t in range(NT) if near[t] and par[t]))
+    print("light-plane skip triangles", [t for t in range(NT) if near[t] and par[t]])
+
+    cam, _, _ = rt.camera_default(a.W, a.H)
+    ip = np.array(cam.inv_projection, np.float64).reshape(4, 4).T   # column-major -> row form
+    iv = np.array(cam.inv_view, np.float64).reshape(4, 4).T
+    cpos = np.array(cam.position, np.float64)
+
+    rng = np.random.default_rng(a.seed)
+    NL = 64 * a.waves
+    tiles_x = a.W // 8
+    tiles_y = a.H // 8
+    tile = rng.integers(0, tiles_x * tiles_y, a.waves)
+    lane = np.arange(NL) % 64
+    w = np.arange(NL) // 64
+    px = (tile[w] % tiles_x) * 8 + (lane & 7)
+    py = (tile[w] // tiles_x) * 8 + (lane >> 3)
+
+    def camera_rays(idx):
+        n = idx.size
+        ux = rng.random(n); uy = rng.random(n)
+        cx = (px[idx] + ux) / a.W * 2 - 1
+        cy = (py[idx] + uy) / a.H * 2 - 1
+        v = np.stack([cx, cy, np.ones(n), np.ones(n)], 1) @ ip.T
+        d = v[:, :3] / v[:, 3:4]
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        wd = np.concatenate([d, np.zeros((n, 1))], 1) @ iv.T
+        d = wd[:, :3]
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        return np.broadcast_to(cpos, (n, 3)).copy(), d
+
+    def mt_all(o, d):
+        """(n, NT): t of the hit (inf on a miss), barycentrics b2, b3, |cos| of the ray with the triangle"""
+        S = o[:, None, :] - A[None]
+        S1 = np.cross(d[:, None, :], E2[None])
+        S2 = np.cross(S, E1[None])
+        den = np.einsum("nij,ij->ni", S1, E1)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            inv = 1.0 / den
+            t = np.einsum("nij,ij->ni", S2, E2) * inv
+            b2 = np.einsum("nij,nij->ni", S1, S) * inv
+            b3 = np.einsum("nij,nj->ni", S2, d) * inv
+        cos = np.abs(d @ (NRM / np.linalg.norm(NRM, axis=1, keepdims=True)).T)
+        return t, b2, b3, cos
+
+    def boxes_hit(o, d):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            r = 1.0 / d
+            t0 = (BLO[None] - o[:, None, :]) * r[:, None, :]
+            t1 = (BHI[None] - o[:, None, :]) * r[:, None, :]
+        tin = np.max(np.minimum(t0, t1), axis=2)
+        tout = np.min(np.maximum(t0, t1), axis=2)
+        hit = (tout >= 0) & (tin <= tout)
+        return hit, tin
+
+    def cand_mask(hit):
+        m = np.zeros(hit.shape[0], np.uint64)
+        for b in range(NB):
+            m |= np.where(hit[:, b], BM[b], np.uint64(0))
+        return m
+
+    def popc(m):
+        m = m.copy()
+        c = np.zeros(m.shape, np.int64)
+        for _ in range(64):
+            c += (m & np.uint64(1)).astype(np.int64)
+            m >>= np.uint64(1)
+        return c
+
+    def bits(m, t):
+        return ((m >> np.uint64(t)) & np.uint64(1)).astype(bool)
+
+    # lane state
+    in_path = np.zeros(NL, bool)
+    o = np.zeros((NL, 3)); dA = np.zeros((NL, 3)); dB = np.zeros((NL, 3))
+    hasA = np.zeros(NL, bool); hasB = np.zeros(NL, bool)
+    slen = np.zeros(NL); sc2 = np.zeros(NL)
+    stats = {k: [] for k in ["lanesA", "lanesB", "nA", "nB", "L0", "L_Aonly", "L_Bonly", "sel_min_tin", "L_mayhit", "L_2phase", "L_2phase_B", "L_tcullA_box", "mayA", "mayB", "survA", "survB"]}
+    for it in range(a.iters):
+        # new camera rays for lanes without a path
+        new = ~in_path
+        idx = np.nonzero(new)[0]
+        # a lane's next path: a pixel anywhere in the image (the kernel's waves hold items of many
+        # tiles, handed out over time; a lane's share of time on a pixel follows its path lengths)
+        px[idx] = rng.integers(0, a.W, idx.size); py[idx] = rng.integers(0, a.H, idx.size)
+        co, cd = camera_rays(idx)
+        o[idx] = co; dA[idx] = cd; hasA[idx] = True; hasB[idx] = False; in_path[idx] = True
+        # trace
+        hitA, tinA = boxes_hit(o, dA)
+        hitB, tinB = boxes_hit(o, dB)
+        ca = np.where(hasA, cand_mask(hitA), np.uint64(0))
+        skip = np.where(sc2 >= 0.25, skipmask, np.uint64(0))
+        cb = np.where(hasB, cand_mask(hitB) & ~skip, np.uint64(0))
+        tA, b2A, b3A, cosA = mt_all(o, dA)
+        tB, b2B, b3B, cosB = mt_all(o, dB)
+        hitTA = (tA > 0) & (b2A > 0) & (b3A > 0) & (1 - b2A - b3A > 0)
+        hitTB = (tB > 0) & (b2B > 0) & (b3B > 0) & (1 - b2B - b3B > 0)
+        candA = np.stack([bits(ca, t) for t in range(NT)], 1)
+        candB = np.stack([bits(cb, t) for t in range(NT)], 1)
+        # closest hit of A among candidates
+        tAc = np.where(candA & hitTA, tA, np.inf)
+        best = np.argmin(tAc, axis=1)
+        bestt = tAc[np.arange(NL), best]
+        anyhit = np.isfinite(bestt)
+        occl = np.any(candB & hitTB & (tB < slen[:, None] - 0.01), axis=1)
+        # ---- policies
+        nA = popc(ca); nB = popc(cb)
+        # may-hit screen (conservative, margin m on the barycentrics and t)
+        mg = 1e-3
+        mayA = candA & (tA > -mg) & (b2A > -mg) & (b3A > -mg) & (1 - b2A - b3A > -mg)
+        mayB = candB & (tB > -mg) & (b2B > -mg) & (b3B > -mg) & (1 - b2B - b3B > -mg)
+        sureA = candA & (tA > mg) & (b2A > mg) & (b3A > mg) & (1 - b2A - b3A > mg) & (cosA > 0.05)
+        # A: the closest sure hit bounds the closest hit; may-hits beyond it (non-grazing) are culled
+        tsure = np.min(np.where(sureA, tA, np.inf), axis=1)
+        survA = mayA & ~((tA > tsure[:, None] * (1 + 1e-4) + 1e-4) & (cosA > 0.05))
+        # B: a sure block ends the ray; may-hits past slen - 0.01 (non-grazing) cannot block
+        sureblk = np.any(candB & (tB < slen[:, None] - 0.02) & (tB > mg) & (b2B > mg) & (b3B > mg) & (1 - b2B - b3B > mg) & (cosB > 0.05), axis=1)
+        survB = mayB & ~((tB > slen[:, None] - 0.005) & (cosB > 0.05))
+        survB &= ~sureblk[:, None]
+        nsA = survA.sum(1); nsB = survB.sum(1)
+        # A: t-cull by box entry after the nearest candidate box (box-level ordering)
+        tinAt = tinA[:, box_of_tri]   # (NL, NT) each triangle's box entry
+        cullA_box = candA & ~((tinAt > bestt[:, None] * (1 + 1e-4) + 1e-4))
+        nA_box = cullA_box.sum(1)
+
+        # block hull filter: a block's triangles are candidates only if the ray meets the block (its
+        # triangles hit with a margin -- stands for a slightly enlarged oriented-box test)
+        blk = (mesh == 1) | (mesh == 2)
+        def hull(candX, tX, b2X, b3X):
+            mg2 = 1e-2
+            mayX = (tX > -mg2) & (b2X > -mg2) & (b3X > -mg2) & (1 - b2X - b3X > -mg2)
+            keep = candX.copy()
+            for m in (1, 2):
+                mm = mesh == m
+                meets = np.any(mayX[:, mm], axis=1)
+                keep[:, mm] &= meets[:, None]
+            return keep
+        hA = hull(candA, tA, b2A, b3A); hB = hull(candB, tB, b2B, b3B)
+        stats.setdefault("L_hull", []).append(0)
+        stats["L_hull"][-1] = (hA.sum(1) + hB.sum(1)).reshape(a.waves, 64).max(1).mean()
+        hAc = hA & ~((tinAt > bestt[:, None] * (1 + 1e-4) + 1e-4))
+        stats.setdefault("L_hull_tcullA", []).append((hAc.sum(1) + hB.sum(1)).reshape(a.waves, 64).max(1).mean())
+        stats.setdefault("L_union", []).append(((candA | candB).sum(1)).reshape(a.waves, 64).max(1).mean())
+        stats.setdefault("L_union_mayhit", []).append(((mayA | mayB).sum(1)).reshape(a.waves, 64).max(1).mean())
+        stats.setdefault("avg_union", []).append((candA | candB).sum() / max(1, (hasA | hasB).sum()))
+        # plane filter: a box whose triangles are coplanar is a candidate only if the ray crosses that
+        # plane inside the box (expanded by 1e-4)
+        def plane_keep(o_, d_, candX):
+            keep = candX.copy()
+            for b in range(NB):
+                tri_b = [t for t in range(NT) if (int(BM[b]) >> t) & 1]
+                n0 = NRM[tri_b[0]]
+                if not all(np.allclose(NRM[t], n0, atol=1e-6) and abs(n0 @ (A[t] - A[tri_b[0]])) < 1e-6 for t in tri_b):
+                    continue
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    tp = ((A[tri_b[0]] - o_) @ n0) / (d_ @ n0)
+                pp = o_ + tp[:, None] * d_
+                inside = np.all((pp >= BLO[b] - 1e-4) & (pp <= BHI[b] + 1e-4), axis=1) & (tp > -1e-4)
+                for t in tri_b:
+                    keep[:, t] &= inside
+            return keep
+        pA = plane_keep(o, dA, candA); pB = plane_keep(o, dB, candB)
+        stats.setdefault("L_plane", []).append(((pA.sum(1) + pB.sum(1))).reshape(a.waves, 64).max(1).mean())
+        stats.setdefault("avg_plane", []).append((pA.sum() + pB.sum()) / max(1, (hasA | hasB).sum()))
+        # box-granular phase 1: candidate boxes per ray
+        def nbox(hit, has, extra_skip=None):
+            return np.where(has, hit.sum(1), 0)
+        nbA = nbox(hitA, hasA)
+        # B boxes after the light skip: a box whose triangles are all skipped is dropped
+        skipb = np.array([(int(BM[b]) & int(skipmask)) == int(BM[b]) for b in range(NB)])
+        nbB = np.where(hasB, (hitB & ~((sc2 >= 0.25)[:, None] & skipb[None])).sum(1), 0)
+        stats.setdefault("L_boxes", []).append((nbA + nbB).reshape(a.waves, 64).max(1).mean())
+        # running-min survivors for A in DFS order (triangle index order)
+        run = np.full(NL, np.inf)
+        survA_run = np.zeros_like(candA)
+        for t in range(NT):
+            lo = tA[:, t] * (1 - 1e-4) - 1e-4
+            may_t = mayA[:, t]
+            keep = may_t & ~((lo > run) & (cosA[:, t] > 0.05))
+            survA_run[:, t] = keep
+            sure_t = sureA[:, t]
+            run = np.where(sure_t, np.minimum(run, tA[:, t] * (1 + 1e-4) + 1e-4), run)
+        stats.setdefault("L_2phase_run", []).append((survA_run.sum(1) + nsB).reshape(a.waves, 64).max(1).mean())
+        stats.setdefault("nA_boxes", []).append(nbA.sum() / max(1, hasA.sum()))
+        stats.setdefault("nA_hull", []).append(hA.sum() / max(1, hasA.sum()))
+        stats.setdefault("nB_hull", []).append(hB.sum() / max(1, hasB.sum()))
+
+        def wmax(x):
+            return x.reshape(a.waves, 64).max(1)
+        stats["lanesA"].append(hasA.sum() / a.waves); stats["lanesB"].append(hasB.sum() / a.waves)
+        stats["nA"].append(nA.sum() / max(1, hasA.sum())); stats["nB"].append(nB.sum() / max(1, hasB.sum()))
+        stats["L0"].append(wmax(nA + nB).mean())
+        stats["L_Aonly"].append(wmax(nA).mean()); stats["L_Bonly"].append(wmax(nB).mean())
+        stats["L_mayhit"].append(wmax(mayA.sum(1) + mayB.sum(1)).mean())
+        stats["L_2phase"].append(wmax(nsA + nsB).mean())
+        stats["L_2phase_B"].append(wmax(nA + nsB).mean())
+        stats["L_tcullA_box"].append(wmax(nA_box + nB).mean())
+        stats["mayA"].append(mayA.sum() / max(1, hasA.sum())); stats["mayB"].append(mayB.sum() / max(1, hasB.sum()))
+        stats["survA"].append(nsA.sum() / max(1, hasA.sum())); stats["survB"].append(nsB.sum() / max(1, hasB.sum()))
+        stats["sel_min_tin"].append(0)
+        # ---- service: advance paths
+        hitA_tri = np.where(hasA & anyhit, best, -1)
+        ends = in_path & (~hasA | (hitA_tri < 0) | emissive[np.maximum(hitA_tri, 0)])
+        in_path &= ~ends
+        hasA[:] = False; hasB[:] = False
+        v = np.nonzero(in_path)[0]
+        if v.size:
+            tri = hitA_tri[v]
+            loc = o[v] + bestt[v, None] * dA[v]
+            N = NRM[tri]
+            wo = -dA[v]
+            n = np.where((np.sum(N * wo, 1) < 0)[:, None], -N, N)
+            p = loc + n * 1e-5
+            # light sample
+            lt = ltris[(rng.random(v.size) >= 0.5).astype(int)]
+            u1 = rng.random(v.size); u2 = rng.random(v.size)
+            x = 1 - np.sqrt(u1); y = u2
+            q = x[:, None] * A[lt] + ((1 - x) * y)[:, None] * B[lt] + ((1 - x) * (1 - y))[:, None] * Cc[lt]
+            p2q = q - p
+            sl = np.linalg.norm(p2q, axis=1)
+            wl = p2q / sl[:, None]
+            nl0 = NRM[lt]
+            nl = np.where((np.sum(nl0 * -wl, 1) < 0)[:, None], -nl0, nl0)
+            c1 = np.sum(wl * n, 1); c2 = np.sum(-wl * nl, 1)
+            hb = c1 > 0
+            o[v] = p; dB[v] = wl; hasB[v] = hb; slen[v] = sl; sc2[v] = c2
+            cont = rng.random(v.size) < 0.8
+            z = rng.random(v.size); phi = 2 * np.pi * rng.random(v.size)
+            r = np.sqrt(np.maximum(0, 1 - z * z))
+            loc3 = np.stack([r * np.cos(phi), r * np.sin(phi), z], 1)
+            Y = np.where((np.abs(n[:, 0]) > np.abs(n[:, 1]))[:, None],
+                         np.stack([n[:, 2], np.zeros(v.size), -n[:, 0]], 1), np.stack([np.zeros(v.size), n[:, 2], -n[:, 1]], 1))
+            Y /= np.linalg.norm(Y, axis=1, keepdims=True)
+            X = np.cross(Y, n)
+            wi = loc3[:, 0:1] * X + loc3[:, 1:2] * Y + loc3[:, 2:3] * n
+            wi /= np.linalg.norm(wi, axis=1, keepdims=True)
+            dA[v] = wi
+            hasA[v] = cont
+            # a path whose roulette stopped still traces its shadow ray this iteration, then ends
+            # (modelled: it stays in_path for the iteration; service ends it since hasA is false)
+    print(f"{a.waves} waves x {a.iters} iterations (first 5 skipped)")
+    for k, vals in stats.items():
+        if k == "sel_min_tin":
+            continue
+        print(f"  {k:14s} {np.mean(vals[5:]):8.3f}")
+
+
+if __name__ == "__main__":
+    main()
