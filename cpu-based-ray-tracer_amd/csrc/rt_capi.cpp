@@ -85,10 +85,15 @@ struct rt_ctx {
     // per lane, into about items_per_lane items per lane but no chunk shorter than min_chunk_frames
     // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
     uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 8;
-    uint64_t lbuf_budget = 32ull << 30;   // bytes of parked samples per launch; C4 needs 25 GB of 288
+    uint64_t lbuf_budget = 96ull << 30;   // bytes of parked samples (+ camera records) per launch; C4 needs 59 GB of 288
     bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(32 GB, 3/4 of free memory) per render
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
+    // the vertex kernel's camera pre-pass: surface-hit records, per-segment counts, the non-empty segments
+    float4* d_crec = nullptr;
+    size_t crec_quads = 0;
+    uint32_t *d_ccount = nullptr, *d_seg_list = nullptr;
+    size_t seg_words = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
@@ -445,6 +450,7 @@ void rt_destroy(rt_ctx* c)
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
     dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf);
+    dfree(c->d_crec); dfree(c->d_ccount); dfree(c->d_seg_list);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev3) (void)hipEventDestroy(c->ev3);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
@@ -665,9 +671,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
     // any other path scene: its BVH variant, the scene in HBM (RT_VERTEX_BVH=0: the megakernel)
     const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
-    // (the BVH variant keeps the hit triangle's material beside its index: < 2^24 triangles, < 128 materials)
-    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 24) &&
-                         P.n_mats < 128u;
+    // (the camera pre-pass's records carry a triangle index in 19 bits, rt_kernels.h crec)
+    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 19);
     const bool coh = coh_box || coh_bvh;
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
@@ -735,10 +740,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 // at most 32 GB, at most 3/4 of what is free
                 size_t fr = 0, tot = 0;
                 HIPC(c, hipMemGetInfo(&fr, &tot));
-                c->lbuf_budget = std::max<uint64_t>(64ull << 20, std::min<uint64_t>(32ull << 30, (fr + c->lbuf_floats * sizeof(float)) / 4 * 3));
+                c->lbuf_budget = std::max<uint64_t>(64ull << 20, std::min<uint64_t>(96ull << 30, (fr + c->lbuf_floats * sizeof(float) + c->crec_quads * sizeof(float4)) / 4 * 3));
             }
             if (want > 1 || park_all) {
-                const uint64_t bytes = px_local * (uint64_t)p->n_frames * 12ull;
+                // parked samples (12 B); the vertex kernel's camera records too (16 B)
+                const uint64_t bytes = px_local * (uint64_t)p->n_frames * (coh ? 28ull : 12ull);
                 passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
             }
             uint32_t done = 0;
@@ -771,13 +777,42 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
                 HIPC(c, hipMemsetAsync(c->d_counters + 3, 0, sizeof(unsigned long long), c->stream));   // this pass's overflow list
+                if (coh) {
+                    // segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
+                    uint32_t lf = 0;
+                    while ((1u << lf) < nf && lf < 6) ++lf;
+                    Q.seg_frames = 1u << lf;
+                    Q.seg_shift = 6 + lf;
+                    Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
+                    const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);
+                    if (nseg >= (1ull << (32 - Q.seg_shift))) { c->err = "too many samples for one pass"; return RT_ERR_INVALID; }
+                    Q.n_segments = (uint32_t)nseg;
+                    if ((nseg << Q.seg_shift) > c->crec_quads) {
+                        HIPC(c, hipStreamSynchronize(c->stream));
+                        dfree(c->d_crec);
+                        c->crec_quads = 0;
+                        HIPC(c, hipMalloc((void**)&c->d_crec, (size_t)(nseg << Q.seg_shift) * sizeof(float4)));
+                        c->crec_quads = (size_t)(nseg << Q.seg_shift);
+                    }
+                    if (nseg > c->seg_words) {
+                        HIPC(c, hipStreamSynchronize(c->stream));
+                        dfree(c->d_ccount); dfree(c->d_seg_list);
+                        c->seg_words = 0;
+                        HIPC(c, hipMalloc((void**)&c->d_ccount, (size_t)nseg * 4));
+                        HIPC(c, hipMalloc((void**)&c->d_seg_list, (size_t)nseg * 4));
+                        c->seg_words = (size_t)nseg;
+                    }
+                    Q.crec = c->d_crec; Q.ccount = c->d_ccount; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
+                    Q.n_chunks = (uint32_t)(nseg / Q.n_tiles);
+                    HIPC(c, rt_launch_camera_prepass(Q, coh_bvh, coh_bvh ? 0 : (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4), c->stream));
+                }
                 if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
                 // EXACT vertex kernel: the samples whose path outgrew the ring, rendered again into their
                 // parked slots (exits at once when none was listed)
                 if (coh && exact) HIPC(c, rt_launch_resample(Q, c->rs_threads, c->stream));
                 HIPC(c, rt_launch_finalize_chunks(Q, (uint32_t)px_local, c->stream));
-                c->stats.n_chunks = n_chunks;
+                c->stats.n_chunks = Q.n_chunks;
                 done += nf;
             }
             c->stats.n_passes = passes;

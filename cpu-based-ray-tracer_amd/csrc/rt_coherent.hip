@@ -100,15 +100,16 @@ struct VertexRng {
         fd.i = 0;
         dim += 6u;
     }
-    // the camera draws: dims 0 and 1 of block 0 (the block is kept in LDS only for unlit scenes,
-    // whose vertices draw through next())
-    __device__ __forceinline__ void camera_draws(uint32_t px, uint32_t fr, bool keep, float& ux, float& uy)
+    // a new sample (pixel, frame) whose camera draws (dims 0 and 1, camera_prepass_kernel) are taken:
+    // the vertices continue at dim 2; an unlit scene's vertices draw through next(), which finds dims 2
+    // and 3 in the block kept in LDS
+    __device__ __forceinline__ void start(uint32_t px, uint32_t fr, bool unlit)
     {
-        uint32_t o[4];
-        philox4x32_10(px, fr, 0u, 0u, k0, k1, o);
-        if (keep) { w[VS_RNG * 256u] = o[0]; w[(VS_RNG + 1) * 256u] = o[1]; w[(VS_RNG + 2) * 256u] = o[2]; w[(VS_RNG + 3) * 256u] = o[3]; }
-        ux = (float)o[0] / 4294967296.0f;
-        uy = (float)o[1] / 4294967296.0f;
+        if (unlit) {
+            uint32_t o[4];
+            philox4x32_10(px, fr, 0u, 0u, k0, k1, o);
+            w[VS_RNG * 256u] = o[0]; w[(VS_RNG + 1) * 256u] = o[1]; w[(VS_RNG + 2) * 256u] = o[2]; w[(VS_RNG + 3) * 256u] = o[3];
+        }
         dim = 2;
     }
 };
@@ -147,6 +148,18 @@ __device__ __forceinline__ bool box_hit_pk(const f2 sx, const f2 sy, const f2 sz
     return (tout >= 0.0f) && (tin <= tout);
 }
 
+// a finished sample's radiance into its parked slot (4-frame blocks: the 4 frames of a block of one pixel
+// are 48 contiguous bytes); finalize_chunks_kernel accumulates every pixel's samples in frame order
+template <class KP>
+__device__ __forceinline__ void park_sample(KP& Q, V3 L, uint32_t local, uint32_t fidx)
+{
+    const size_t blk = Q.lbuf_pixel_major ? (size_t)local * ((Q.n_frames + 3u) >> 2) + (fidx >> 2) : (size_t)(fidx >> 2) * Q.lbuf_stride + local;
+    const size_t at = (blk * 4u + (fidx & 3u)) * 3u;
+    Q.lbuf[at] = L.x;
+    Q.lbuf[at + 1] = L.y;
+    Q.lbuf[at + 2] = L.z;
+}
+
 __device__ __forceinline__ V3 rcp3(V3 d) { return V3{rcp_f32(d.x), rcp_f32(d.y), rcp_f32(d.z)}; }
 __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
@@ -179,13 +192,10 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #define RT_SEC_COUNTS 20
 
 // Tuned constants (A/B history: DESIGN.md 6.4, profiles/r02/ab/):
-//  * work items per refill of a wave's pool from the device counter (<= 64: a wave's pool never holds
-//    more than one item per lane, so the launch tail stays one item long);
 //  * leaf boxes per scalar-load group in the box loop (one wait per 4 boxes; +0.9 % C4 over 1);
 //  * fold levels drained per iteration at the top of the loop, their ring loads issued together (a fold
 //    then rarely still drains when the next path ends): C4 1 level 5935, 2 6117, 3 6198, 4 6195 Msamples/s;
 //  * ring levels loaded together when a fold is completed at once (drain_all).
-constexpr uint32_t WQ_BATCH = 64u;
 constexpr int BOX_UNROLL = 4;
 constexpr uint32_t DRAIN_STEP = 3;
 constexpr uint32_t DRAIN_BATCH = 2;
@@ -260,15 +270,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // after a store of the same iteration: on gfx950 a load waits for every older store of its wave
     // (vmcnt counts both), and a path-tracing iteration that read the accumulator after its parked
     // samples and fold-level stores waited for their write-back.
-    auto complete = [&](V3 L, uint32_t local, uint32_t fidx) {
-        CKParams& Q = kargs4();
-        const size_t blk = Q.lbuf_pixel_major ? (size_t)local * ((Q.n_frames + 3u) >> 2) + (fidx >> 2)
-                                              : (size_t)(fidx >> 2) * Q.lbuf_stride + local;
-        const size_t at = (blk * 4u + (fidx & 3u)) * 3u;
-        Q.lbuf[at] = L.x;
-        Q.lbuf[at + 1] = L.y;
-        Q.lbuf[at + 2] = L.z;
-    };
+    auto complete = [&](V3 L, uint32_t local, uint32_t fidx) { park_sample(kargs4(), L, local, fidx); };
     // up to N fold steps of the draining path, L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
     // (MC/Renderer.cpp:208,213), inner level first, from ring position `pos` down; the N ring loads are
     // issued together (levels past the fold re-read the first one, unused).  Returns the levels folded.
@@ -317,15 +319,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         complete(L, lsu(VS_DT0), lsu(VS_DT1));
     };
 
-    bool alive = true, have_pixel = false, in_path = false;
-    uint32_t k = 0;       // frame of the current item (item of chunk c: frames c * chunk_frames + [0, kend))
+    bool alive = true, in_path = false;
     uint32_t depth = 0;   // vertices shaded so far on this path
-    bool pend = false;    // vertex depth-1 waits for its shadow verdict (and its indirect hit when cont)
-    bool cont = false;    // vertex depth-1's roulette continued: ray A is its indirect ray
+    bool cont = false;    // the last vertex's roulette continued: ray A is its indirect ray
     VertexRng g;
     g.w = reinterpret_cast<uint32_t*>(lstate) + tib;
     g.k0 = (uint32_t)P.seed; g.k1 = (uint32_t)(P.seed >> 32);
-    // the lane's rays: A = camera or indirect ray (closest hit), B = shadow ray (any hit); shared origin
+    // the lane's rays: A = indirect ray (closest hit), B = shadow ray (any hit); shared origin.  Camera rays
+    // are traced by the pre-pass (camera_prepass_kernel): a path starts here at its first surface vertex.
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
@@ -333,18 +334,21 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
     int triA = -1;                            // closest triangle
     bool occB = false;                        // shadow ray blocked
-    // EXACT: a finished path's levels are folded one per iteration ("drain"), not in a loop at the end of
-    // the path: lanes end paths of different depths, and a fold loop runs as long as the deepest one.
-    // Levels live in a per-lane ring of stack_depth positions in HBM ([position][thread]); the next path
-    // pushes above the draining segment.  A sample is accumulated when its fold completes; a path that
-    // ends while the previous fold still drains first completes that fold, so the per-pixel order of the
-    // accumulation is the frame order.
+    // EXACT: a finished path's levels are folded DRAIN_STEP per iteration ("drain"), not in a loop at the
+    // end of the path: lanes end paths of different depths, and a fold loop runs as long as the deepest
+    // one.  Levels live in a per-lane ring of stack_depth positions in HBM; the next path pushes above the
+    // draining segment.  Every sample has its own parked slot, which finalize_chunks_kernel adds in frame
+    // order.
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
-    uint32_t pool_base = 0, pool_count = 0;   // the wave's batch of work items (wave-uniform)
     if (EXACT) lsu(VS_BASE) = 0u;
     // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
     const uint32_t NN = S.n_nodes;
     uint32_t tiA = NN, tiB = NN;
+    // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
+    // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
+    uint32_t seg_pos = 0, seg_end = 0;
+    const uint32_t n_list = __builtin_amdgcn_readfirstlane(*P.seg_list_n);
+    bool list_left = true;
 
 #if RT_SECTIONS
     uint64_t sec_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -365,243 +369,138 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #define SEC_SUM(i, v) do { } while (0)
 #define SEC_MARK(k) do { } while (0)
 #endif
-    // Lanes without a work item take the next ones from the wave's pool, in lane order.  With `refill`
-    // (the top of the iteration, before any store) an empty pool is refilled from the device counter;
-    // without it (after the path-end block, so a lane whose item just ended starts the
-    // next one's camera ray in the same iteration) only the pool's items are handed out -- no atomic,
-    // so nothing waits for the iteration's stores.
-    auto take_items = [&](const bool refill) {
-        const bool need = alive && !have_pixel;
-        const uint64_t mask = __ballot(need);
-        if (mask == 0) return;
-        CKParams& Q = kargs4();
-        uint32_t n = (uint32_t)__popcll(mask);
-        if (!refill && n > pool_count) n = pool_count;
-        if (n == 0) return;
-        uint32_t fresh = 0;   // first item of a new batch (wave-uniform)
-        if (n > pool_count) {
-            uint32_t b = 0;
-            if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, WQ_BATCH);
-            fresh = __builtin_amdgcn_readfirstlane(b);
-        }
-        const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-        if (need && j < n) {
-            const uint32_t w = j < pool_count ? pool_base + j : fresh + (j - pool_count);
-            if (w >= Q.n_items) {
-                alive = false;
-            } else {
-                // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
-                const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
-                const uint32_t tile = wp >> 6, within = wp & 63u;
-                const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
-                const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
-                if (lr < Q.n_local_rows && lx < Q.W) {
-                    // local row -> global row (row bands dealt round-robin over ranks)
-                    const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
-                    const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
-                    const uint32_t local = lr * Q.W + lx;
-                    lsu(VS_LOCAL) = local;
-                    lsu(VS_PIX) = y * Q.W + lx;
-                    lsu(VS_FRAME) = Q.first_frame + c * Q.chunk_frames;   // the frame of the item's first sample
-                    have_pixel = true;
-                    k = 0;
-                }
+    // Lanes that need a sample take the wave's next records, in lane order (wave-collective); returns the
+    // lane's record index or NO_REC.  Called at the top of the iteration, before any store: the record
+    // loads (and the segment fetch's returning atomic) then wait for no store of the iteration.
+    constexpr uint32_t NO_REC = 0xFFFFFFFFu;
+    auto take_records = [&](const bool need) -> uint32_t {
+        uint32_t rec = NO_REC;
+        uint64_t mask = __ballot(need);
+        while (mask != 0) {
+            if (seg_pos == seg_end) {
+                if (!list_left) break;
+                CKParams& Q = kargs4();
+                uint32_t k = 0;
+                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
+                k = __builtin_amdgcn_readfirstlane(k);
+                if (k >= n_list) { list_left = false; break; }
+                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k]);
+                seg_pos = sg << Q.seg_shift;
+                seg_end = seg_pos + __builtin_amdgcn_readfirstlane(Q.ccount[sg]);
+                continue;
             }
+            const uint32_t avail = seg_end - seg_pos;
+            const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+            if (((mask >> lane) & 1ull) && j < avail) rec = seg_pos + j;
+            const uint32_t n = (uint32_t)__popcll(mask);
+            seg_pos += n < avail ? n : avail;
+            mask = __ballot(need && rec == NO_REC);
         }
-        if (n > pool_count) {
-            pool_base = fresh + (n - pool_count);
-            pool_count = WQ_BATCH - (n - pool_count);
-        } else {
-            pool_base += n;
-            pool_count -= n;
-        }
+        if (need && rec == NO_REC) alive = false;
+        return rec;
     };
     for (;;) {
         SEC_MARK(0);
+        // ======================= the lanes whose path ends in this iteration's service =======================
+        // decided from the trace results before any store: the roulette stopped, or the indirect ray missed or
+        // hit the light (radiance_indirect = 0, MC/Renderer.cpp:193-209).  They and the idle lanes take their
+        // next sample now, so a finishing lane shades its next path's first vertex in the same iteration.
+        const bool served = in_path && (!BVH || (tiA >= NN && tiB >= NN));
+        int mat = 0;
+        bool emissive = false;
+        if (served && hasA && triA >= 0) {
+            mat = f2i(S.tris[4 * triA].w);
+            emissive = S.mats[2 * mat].w != 0.0f;
+        }
+        const bool ends = served && (!cont || triA < 0 || emissive);
+        const uint32_t rid = take_records(alive && (!in_path || ends));
+        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rid != NO_REC) rec = kargs4().crec[rid];
         if (EXACT && __any(dleft != 0u)) {
-            if (dleft != 0u) {
-                drain_step(dleft);
-            }
+            if (dleft != 0u) drain_step(dleft);
         }
         SEC_MARK(3);
-        // ======================= lane-level work queue (wave-collective) =======================
-        // at the top of the iteration, before any store: a lane that finished its item in the previous
-        // iteration takes the next one (the returning atomic waits for no store of this iteration).
-        // The wave takes items from the device counter in batches of WQ_BATCH into a wave-private pool
-        // (two uniform registers); lanes are served from the pool in lane order.  One returning atomic
-        // on one word saturates near 88 dequeues/us (MI355X_MICROARCH.md, dequeue): one per refill
-        // (a lane or two per wave and iteration) was the limit at 16-frame chunks.
-        take_items(true);
 
-        // ======================= service: every lane on a path has its rays back =======================
-        // (BVH: the lanes whose two rays are done)
-        if (in_path && (!BVH || (tiA >= NN && tiB >= NN))) {
+        // ======================= service: the lanes whose rays are back =======================
+        bool vertex = false;   // a surface vertex to shade: the indirect ray's hit, or a new path's camera hit
+        if (served) {
             CKParams& Q = kargs4();
             bool finished = false;
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
             bool relisted = false;   // EXACT: the sample went to the overflow list (no fold, no parked store)
             V3 L{0.f, 0.f, 0.f};
-            int mat = 0;
-            bool emissive = false;
-            if (hasA && triA >= 0) {
-                // BVH variant: the material came with the hit (tri_mat)
-                mat = f2i(S.tris[4 * triA].w);
-                emissive = S.mats[2 * mat].w != 0.0f;
-            }
-            bool vertex = false;
-            if (pend) {
-                // vertex depth-1's direct term (MC/Renderer.cpp:184-189): the shadow verdict
-                V3 ld{0.f, 0.f, 0.f};
-                if (hasB && !occB) ld = ls3(VS_LD);
-                if (!EXACT) {
-                    const V3 thr = ls3(VS_THR);
-                    if (!cont) {
-                        L = add(ls3(VS_LSUM), mul(thr, ld));
-                        finished = true;
-                    } else {
-                        const V3 lsum = add(ls3(VS_LSUM), mul(thr, ld));
-                        st3(VS_LSUM, lsum);
-                        const float c = lsf(VS_PCOS);
-                        const float4 mb = S.mats[2 * lsu(VS_MAT)];
-                        const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
-                        if (triA < 0 || emissive) { L = lsum; finished = true; }
-                        else vertex = true;
-                    }
-                } else if (!cont || triA < 0 || emissive) {
-                    // the roulette stopped, or the indirect ray missed / hit the light
-                    // (radiance_indirect = 0, MC/Renderer.cpp:202): vertex depth-1 ends the path
-                    L = ld;
-                    fold_top = (int)depth - 2;
+            // the last vertex's direct term (MC/Renderer.cpp:184-189): the shadow verdict
+            V3 ld{0.f, 0.f, 0.f};
+            if (hasB && !occB) ld = ls3(VS_LD);
+            if (!EXACT) {
+                const V3 thr = ls3(VS_THR);
+                const V3 lsum = add(ls3(VS_LSUM), mul(thr, ld));
+                if (ends) {
+                    L = lsum;
                     finished = true;
                 } else {
-                    // the indirect ray hit a surface: vertex depth-1 becomes stack level depth-1
-                    const uint32_t lvl = depth - 1;
-                    const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
-                    const uint32_t pm = lsu(VS_MAT);
-                    const uint32_t R = Q.stack_depth;
-                    uint32_t pos = lsu(VS_BASE) + lvl;
-                    if (pos >= R) pos -= R;
-                    // the ring holds this path's levels above the draining ones, which occupy the R positions
-                    // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
-                    bool fits = lvl < R;
-                    if (fits && dleft != 0u) {
-                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
-                        fits = (pos + R - lo) % R >= dleft;
-                    }
-                    if (fits) {
-                        if (Q.ring_pack) {
-                            // the material in the sign bits of the direct term (rt_kernels.h ring_pack)
-                            const float4 pe = make_float4(__uint_as_float((__float_as_uint(e.x) & 0x7FFFFFFFu) | ((pm & 1u) << 31)),
-                                                          __uint_as_float((__float_as_uint(e.y) & 0x7FFFFFFFu) | ((pm & 2u) << 30)),
-                                                          __uint_as_float((__float_as_uint(e.z) & 0x7FFFFFFFu) | ((pm & 4u) << 29)), e.w);
-                            Q.stack_ld[RING_AT(pos)] = pe;
-                        } else {
-                            Q.stack_ld[RING_AT(pos)] = e;
-                            Q.stack_mat[RING_AT(pos)] = pm;
-                        }
-                        vertex = true;
-                    } else {
-                        // the path outgrew the ring: list the sample for the exact re-render
-                        // (rt_resample.hip) and end it here; its parked slot is written there
-                        const uint32_t slot = (uint32_t)atomicAdd((unsigned long long*)&Q.counters[3], 1ull);
-                        atomicAdd((unsigned long long*)&Q.counters[14], 1ull);
-                        const uint32_t frame = lsu(VS_FRAME);
-                        if (slot < Q.ovf_cap) Q.ovf_list[slot] = make_uint4(lsu(VS_LOCAL), frame - Q.first_frame, lsu(VS_PIX), frame);
-                        else atomicAdd((unsigned long long*)&Q.counters[13], 1ull);   // lost: rt_render reports it
-                        finished = true;
-                        relisted = true;
-                    }
+                    st3(VS_LSUM, lsum);
+                    const float c = lsf(VS_PCOS);
+                    const float4 mb = S.mats[2 * lsu(VS_MAT)];
+                    const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
+                    st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
+                    vertex = true;
                 }
-            } else if (triA < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
-                L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
-                finished = true;
-            } else if (emissive) {   // direct emission (MC/Renderer.cpp:151-161)
-                const float4 em = S.mats[2 * mat + 1];
-                L = V3{em.x, em.y, em.z};
+            } else if (ends) {
+                L = ld;
+                fold_top = (int)depth - 2;
                 finished = true;
             } else {
-                vertex = true;
+                // the indirect ray hit a surface: vertex depth-1 becomes stack level depth-1
+                const uint32_t lvl = depth - 1;
+                const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
+                const uint32_t pm = lsu(VS_MAT);
+                const uint32_t R = Q.stack_depth;
+                uint32_t pos = lsu(VS_BASE) + lvl;
+                if (pos >= R) pos -= R;
+                // the ring holds this path's levels above the draining ones, which occupy the R positions
+                // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
+                bool fits = lvl < R;
+                if (fits && dleft != 0u) {
+                    const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
+                    fits = (pos + R - lo) % R >= dleft;
+                }
+                if (fits) {
+                    if (Q.ring_pack) {
+                        // the material in the sign bits of the direct term (rt_kernels.h ring_pack)
+                        const float4 pe = make_float4(__uint_as_float((__float_as_uint(e.x) & 0x7FFFFFFFu) | ((pm & 1u) << 31)),
+                                                      __uint_as_float((__float_as_uint(e.y) & 0x7FFFFFFFu) | ((pm & 2u) << 30)),
+                                                      __uint_as_float((__float_as_uint(e.z) & 0x7FFFFFFFu) | ((pm & 4u) << 29)), e.w);
+                        Q.stack_ld[RING_AT(pos)] = pe;
+                    } else {
+                        Q.stack_ld[RING_AT(pos)] = e;
+                        Q.stack_mat[RING_AT(pos)] = pm;
+                    }
+                    vertex = true;
+                } else {
+                    // the path outgrew the ring: list the sample for the exact re-render
+                    // (rt_resample.hip) and end it here; its parked slot is written there
+                    const uint32_t slot = (uint32_t)atomicAdd((unsigned long long*)&Q.counters[3], 1ull);
+                    const uint32_t frame = lsu(VS_FRAME);
+                    if (slot < Q.ovf_cap) {
+                        Q.ovf_list[slot] = make_uint4(lsu(VS_LOCAL), frame - Q.first_frame, lsu(VS_PIX), frame);
+                        atomicAdd((unsigned long long*)&Q.counters[14], 1ull);
+                    } else {
+                        atomicAdd((unsigned long long*)&Q.counters[13], 1ull);   // lost: rt_render reports it
+                    }
+                    finished = true;
+                    relisted = true;
+                }
             }
-
             SEC_MARK(1);
 #if RT_SECTIONS
-            dbg_vertex = vertex; dbg_fin = finished;
+            dbg_fin = finished;
 #endif
-            if (vertex) {
-                // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
-                const int ti3 = triA;
-                const float4 tq3 = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[ti3] : S.tris[4 * ti3 + 3];
-                const V3 wo = neg(dA);
-                const V3 loc = add(o, smul((float)tA, dA));   // Ray::operator(), MC/Ray.h:34-37
-                const V3 N{tq3.x, tq3.y, tq3.z};
-                const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
-                const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
-                auto shade = [&](auto& G) {
-                    hasB = false;
-                    if (Q.has_light) {
-                        V3 q, nl0;
-                        uint32_t lskip = 0;
-                        sample_light(S, Q.light_area, G, q, nl0, &lskip);
-                        const V3 p2q = sub(q, p);
-                        const V3 wl = glm_normalize(p2q);
-                        const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
-                        const float sc1 = dot(wl, n), sc2 = dot(neg(wl), nl), sd2 = dot(p2q, p2q);
-                        slen = glm_length(p2q);
-                        // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
-                        const float4 mb = S.mats[2 * mat];
-                        const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                        const V3 ldu = vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
-                                                 BVH ? 0.0f : rcp_f32(sd2)),
-                                            Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
-                        st3(VS_LD, ldu);
-                        dB = wl;
-                        // a zero unoccluded term (the light behind the surface: f = 0) makes the verdict pick
-                        // between +0 and +-0, which no accumulation can tell apart (sums start at +0): no
-                        // shadow ray then (the direct term is taken as +0, as for an occluded light)
-                        hasB = !(ldu.x == 0.0f && ldu.y == 0.0f && ldu.z == 0.0f);
-                        // triangles (near-)coplanar with the sampled light triangle are hit, if at all, within
-                        // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
-                        // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
-                        if (NARROW && !BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
-                    }
-                    // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
-                    cont = G.next() < Q.rr && depth < 4096u;
-                    if (cont) {
-                        const V3 wi = glm_normalize(sample_hemisphere(n, G));
-                        lsf(VS_PCOS) = dot(wi, n);
-                        lsu(VS_MAT) = (uint32_t)mat;
-                        dA = wi;
-                    }
-                };
-                if (Q.has_light) {
-                    FixedDraws fd;
-                    g.vertex_draws(fd);
-                    shade(fd);
-                } else {
-                    shade(g);
-                }
-                hasA = cont;
-                o = p;
-                pend = true;
-                depth = depth + 1;
-                if (BVH) {
-                    tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
-                    tA = 1.7976931348623157e308; triA = -1; occB = false;
-                }
-            }
-
-            SEC_MARK(2);
             if (finished) {
                 in_path = false;
                 hasA = hasB = false;
-                const uint32_t local = lsu(VS_LOCAL), frame = lsu(VS_FRAME);
-                const uint32_t fidx = frame - Q.first_frame;   // the sample's frame index in this launch
-                const uint32_t kbase = fidx - k;               // the item's first frame index
-                ++k;
-                lsu(VS_FRAME) = frame + 1u;
-                const bool last = k == min(Q.chunk_frames, Q.n_frames - kbase);
-                if (last) have_pixel = false;
+                const uint32_t local = lsu(VS_LOCAL);
+                const uint32_t fidx = lsu(VS_FRAME) - Q.first_frame;   // the sample's frame index in this launch
                 if (EXACT && relisted) {
                     // nothing to fold or park: resample_kernel writes this sample's slot
                 } else if (EXACT) {
@@ -632,41 +531,113 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 }
             }
         }
-
-        take_items(false);
         SEC_MARK(4);
-        // ======================= new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
-        if (have_pixel && !in_path) {
+
+        // ======================= the vertex to shade: (location, triangle, face-forward) =======================
+        V3 loc;
+        int tri;
+        bool flip;
+        if (rid != NO_REC) {
+            // a new path from its camera-hit record: sample (pixel, frame) from the segment and the tag
+            // (rt_kernels.h crec), the location and face-forwarded normal as the pre-pass computed them
             CKParams& Q = kargs4();
-            const uint32_t pix = lsu(VS_PIX), y = pix / Q.W, x = pix - y * Q.W;
-            float ux, uy;
-            g.camera_draws(pix, lsu(VS_FRAME), !Q.has_light, ux, uy);
+            const uint32_t tag = __float_as_uint(rec.w);
+            const uint32_t sg = rid >> Q.seg_shift;
+            const uint32_t c = sg / Q.n_tiles, tile = sg - c * Q.n_tiles;
+            const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
+            const uint32_t pit = (tag >> 19) & 63u;
+            const uint32_t lr = trow * 8u + (pit >> 3), lx = tcol * 8u + (pit & 7u);
+            // local row -> global row (row bands dealt round-robin over ranks)
+            const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+            const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
+            const uint32_t pix = y * Q.W + lx;
+            const uint32_t frame = Q.first_frame + c * Q.seg_frames + ((tag >> 25) & 63u);
+            lsu(VS_LOCAL) = lr * Q.W + lx;
+            lsu(VS_PIX) = pix;
+            lsu(VS_FRAME) = frame;
+            g.start(pix, frame, !Q.has_light);   // the vertex draws continue after the 2 camera draws
+            loc = V3{rec.x, rec.y, rec.z};
+            tri = (int)(tag & 0x7FFFFu);
+            flip = (tag >> 31) != 0u;
+            mat = f2i(S.tris[4 * tri].w);
+            depth = 0;
+            in_path = true;
+            vertex = true;
+            if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
 #if RT_SECTIONS
             dbg_cam = true;
 #endif
-            float cx = sdiv((float)x + ux, (float)Q.W, Q.y_w);
-            float cy = sdiv((float)y + uy, (float)Q.H, Q.y_h);
-            cx = cx * 2.0f - 1.0f;
-            cy = cy * 2.0f - 1.0f;
-            float tg[4];
-            mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
-            float wd[4];
-            mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
-            o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
-            dA = w_normalize(V3{wd[0], wd[1], wd[2]});
-            hasA = true; hasB = false;
-            depth = 0;
-            pend = false;
-            in_path = true;
+        } else {
+            // the indirect ray's hit: Ray::operator() (MC/Ray.h:34-37) and the face-forward against -dA
+            tri = triA;
+            loc = add(o, smul((float)tA, dA));
+            const float4 tn = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[tri < 0 ? 0 : tri] : S.tris[4 * (tri < 0 ? 0 : tri) + 3];
+            flip = dot(V3{tn.x, tn.y, tn.z}, neg(dA)) < 0.0f;
+        }
+#if RT_SECTIONS
+        dbg_vertex = vertex;
+#endif
+        if (vertex) {
+            // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
+            CKParams& Q = kargs4();
+            const float4 tq3 = (BVH && Q.use_qnodes) ? Q.tnrm[tri] : S.tris[4 * tri + 3];
+            const V3 N{tq3.x, tq3.y, tq3.z};
+            const V3 n = flip ? neg(N) : N;
+            const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
+            auto shade = [&](auto& G) {
+                hasB = false;
+                if (Q.has_light) {
+                    V3 q, nl0;
+                    uint32_t lskip = 0;
+                    sample_light(S, Q.light_area, G, q, nl0, &lskip);
+                    const V3 p2q = sub(q, p);
+                    const V3 wl = glm_normalize(p2q);
+                    const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
+                    const float sc1 = dot(wl, n), sc2 = dot(neg(wl), nl), sd2 = dot(p2q, p2q);
+                    slen = glm_length(p2q);
+                    // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
+                    const float4 mb = S.mats[2 * mat];
+                    const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
+                    const V3 ldu = vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
+                                             BVH ? 0.0f : rcp_f32(sd2)),
+                                        Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
+                    st3(VS_LD, ldu);
+                    dB = wl;
+                    // a zero unoccluded term (the light behind the surface: f = 0) makes the verdict pick
+                    // between +0 and +-0, which no accumulation can tell apart (sums start at +0): no
+                    // shadow ray then (the direct term is taken as +0, as for an occluded light)
+                    hasB = !(ldu.x == 0.0f && ldu.y == 0.0f && ldu.z == 0.0f);
+                    // triangles (near-)coplanar with the sampled light triangle are hit, if at all, within
+                    // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
+                    // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
+                    if (NARROW && !BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
+                }
+                // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
+                cont = G.next() < Q.rr && depth < 4096u;
+                if (cont) {
+                    const V3 wi = glm_normalize(sample_hemisphere(n, G));
+                    lsf(VS_PCOS) = dot(wi, n);
+                    lsu(VS_MAT) = (uint32_t)mat;
+                    dA = wi;
+                }
+            };
+            if (Q.has_light) {
+                FixedDraws fd;
+                g.vertex_draws(fd);
+                shade(fd);
+            } else {
+                shade(g);
+            }
+            hasA = cont;
+            o = p;
+            depth = depth + 1;
             if (BVH) {
-                tiA = 0u; tiB = NN;
+                tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
                 tA = 1.7976931348623157e308; triA = -1; occB = false;
             }
-            if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
         }
 
-        if (!__any(have_pixel || alive)) {
+        if (!__any(in_path || alive)) {
             if (EXACT) drain_all(dleft);
             break;
         }
@@ -850,7 +821,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 const bool tracing = in_path && (tiA < NN || tiB < NN);
                 const uint64_t act = __ballot(tracing);
                 if (act == 0) break;
-                const uint64_t srv = __ballot((in_path && !tracing) || (alive && !have_pixel));
+                const uint64_t srv = __ballot((in_path && !tracing) || (alive && !in_path));
                 if ((uint32_t)__popcll(act) <= thresh && srv != 0) break;
                 const bool curA = tiA < NN;
                 const V3 d = curA ? dA : dB;
@@ -953,6 +924,141 @@ template __global__ void pt_coherent_kernel<true, false, false>(KParams);
 template __global__ void pt_coherent_kernel<false, false, false>(KParams);
 template __global__ void pt_coherent_kernel<true, true, false>(KParams);
 template __global__ void pt_coherent_kernel<false, true, false>(KParams);
+
+// ---------------------------------------------------------------------------------------------
+// The vertex kernel's camera pre-pass.  One wave per segment (an 8x8 tile of local pixels x the segment's
+// frames, rt_kernels.h), one lane per pixel, the frames in order.  Each sample's camera ray
+// (Camera::RecomputeRayDirections, MC/Camera.cpp:114-132, and RayGen_Shader's normalize,
+// MC/Renderer.cpp:128) is traced to its closest hit (cast_path, MC/Renderer.cpp:136-146).  A miss (night
+// sky, :145) or a hit on the light (direct emission, :151-161) is the sample's radiance: it is parked at
+// once.  A surface hit becomes a record -- the hit location (Ray::operator(), MC/Ray.h:34-37) and the
+// face-forward of the triangle's normal against -dir (MC/Renderer.cpp:163-166) -- from which the vertex
+// kernel starts the path at its first vertex.  The camera rays of a tile are coherent, so the candidate
+// loop here runs nearly converged, and the vertex kernel spends no iteration on camera rays or on sky
+// samples.
+template <bool BVH>
+__global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
+    SceneView S;
+    S.n_nodes = P.n_nodes; S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = nullptr;
+    if (!BVH) {   // the small scene's triangles and materials in LDS (the leaf boxes come with scalar loads)
+        const uint32_t tq = 4 * P.n_tris, mq = 2 * P.n_mats;
+        float4* dt = lds_scene;
+        float4* dm = dt + tq;
+        for (uint32_t i = threadIdx.x; i < tq; i += blockDim.x) dt[i] = P.tris[i];
+        for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
+        __syncthreads();
+        S.tris = dt; S.mats = dm;
+    }
+    const uint32_t lane = __lane_id();
+    const uint32_t sg = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (sg >= P.n_segments) return;   // whole waves
+    const uint32_t c = sg / P.n_tiles, tile = sg - c * P.n_tiles;
+    const uint32_t trow = tile / P.tiles_x, tcol = tile - trow * P.tiles_x;
+    const uint32_t lr = trow * 8u + (lane >> 3), lx = tcol * 8u + (lane & 7u);
+    const bool valid = lr < P.n_local_rows && lx < P.W;
+    // local row -> global row (row bands dealt round-robin over ranks)
+    const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
+    const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
+    const uint32_t pix = y * P.W + lx, local = lr * P.W + lx;
+    const uint32_t f0 = c * P.seg_frames;
+    const uint32_t nf = min(P.seg_frames, P.n_frames - f0);
+    const V3 o{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
+    float4* const out = P.crec + ((size_t)sg << P.seg_shift);
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < nf; ++j) {
+        const uint32_t fidx = f0 + j, frame = P.first_frame + fidx;
+        // the camera ray: the two camera draws (dims 0, 1 of the sample's stream), jitter, NDC,
+        // inverse projection, normalize(xyz / w), inverse view, then Whitted::normalize
+        uint32_t ow[4];
+        philox4x32_10(pix, frame, 0u, 0u, (uint32_t)P.seed, (uint32_t)(P.seed >> 32), ow);
+        const float ux = (float)ow[0] / 4294967296.0f, uy = (float)ow[1] / 4294967296.0f;
+        float cx = div_fast((float)lx + ux, (float)P.W, P.y_w);
+        float cy = div_fast((float)y + uy, (float)P.H, P.y_h);
+        cx = cx * 2.0f - 1.0f;
+        cy = cy * 2.0f - 1.0f;
+        float tg[4];
+        mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
+        const V3 dv = glm_normalize(divs_fast(V3{tg[0], tg[1], tg[2]}, tg[3], rcp_f32(tg[3])));
+        float wd[4];
+        mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
+        const V3 d = w_normalize(V3{wd[0], wd[1], wd[2]});
+        const Ray r = make_ray(o, d);
+        // closest hit, the later leaf winning ties (MC/BVH.h:97-100)
+        double t = 1.7976931348623157e308;
+        int tri = -1;
+        bool fin = rcp_finite(r) && P.force_walk == 0u;
+        if (!BVH) {
+            // the distinct leaf boxes decide the candidates (rt_scene.cpp); Moller-Trumbore in DFS order
+            uint64_t cm = 0;
+            cbox8* bx = (cbox8*)P.lboxes;
+            for (uint32_t b = 0; b < P.n_lboxes; ++b) {
+                const box8 q = bx[b];
+                const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
+                const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
+                const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
+                const uint64_t m = (uint64_t)(uint32_t)f2i(q.s6) | ((uint64_t)(uint32_t)f2i(q.s7) << 32);
+                cm |= box_hit_pk(sx, sy, sz, r.rcp) ? m : 0ull;
+            }
+            if (!valid || !fin) cm = 0;
+            while (cm != 0) {
+                const int k = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                const float4* T = S.tris + 4 * k;
+                const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+                double tk;
+                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, tk) && tk <= t) { t = tk; tri = k; }
+            }
+            fin = fin || !valid;
+        } else {
+            fin = __all(!valid || fin);
+        }
+        if (valid && (BVH || !fin)) {
+            // the BVH variant's scene, or a ray with a non-finite reciprocal direction: the stackless walk
+            // (the reference's traversal, rt_path.h)
+            bool occ = false;
+            uint32_t nt = 0, tt = 0;
+            if (fin) traverse_impl<false, true>(S, r, false, 0.0, t, tri, occ, nt, tt);
+            else traverse_impl<false, false>(S, r, false, 0.0, t, tri, occ, nt, tt);
+        }
+        bool surface = false;
+        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (valid) {
+            V3 L{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};   // cast_path miss: night sky (MC/Renderer.cpp:145)
+            if (tri >= 0) {
+                const int mat = f2i(S.tris[4 * tri].w);
+                if (S.mats[2 * mat].w != 0.0f) {   // direct emission (MC/Renderer.cpp:151-161)
+                    const float4 em = S.mats[2 * mat + 1];
+                    L = V3{em.x, em.y, em.z};
+                } else {
+                    surface = true;
+                    const V3 loc = add(o, smul((float)t, d));   // Ray::operator(), MC/Ray.h:34-37
+                    const float4 tn = S.tris[4 * tri + 3];
+                    const bool flip = dot(V3{tn.x, tn.y, tn.z}, neg(d)) < 0.0f;
+                    rec = make_float4(loc.x, loc.y, loc.z, __uint_as_float((uint32_t)tri | (lane << 19) | (j << 25) | (flip ? 0x80000000u : 0u)));
+                }
+            }
+            if (!surface) park_sample(P, L, local, fidx);
+        }
+        const uint64_t hits = __ballot(surface);
+        if (surface) out[cnt + (uint32_t)__popcll(hits & ((1ull << lane) - 1ull))] = rec;
+        cnt += (uint32_t)__popcll(hits);
+    }
+    if (lane == 0) {
+        P.ccount[sg] = cnt;
+        if (cnt != 0u) P.seg_list[atomicAdd(P.seg_list_n, 1u)] = sg;
+    }
+}
+
+hipError_t rt_launch_camera_prepass(const KParams& P, bool bvh, size_t lds, hipStream_t stream)
+{
+    if (P.n_segments == 0) return hipSuccess;
+    const uint32_t blocks = (P.n_segments + 3u) / 4u;
+    if (bvh) hipLaunchKernelGGL(camera_prepass_kernel<true>, dim3(blocks), dim3(256), 0, stream, P);
+    else hipLaunchKernelGGL(camera_prepass_kernel<false>, dim3(blocks), dim3(256), lds, stream, P);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------------------------
 // device checks of the primitives the kernels shortcut (C-ABI rt_debug_primitives): the reference's

@@ -57,6 +57,13 @@ struct KParams {
     uint32_t lds_levels;            // EXACT: the first lds_levels stack levels live in LDS (after the scene)
     uint32_t lds_pad;               // diagnostic: unused dynamic LDS bytes per workgroup (occupancy experiments)
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
+    // the vertex kernel's camera pre-pass (camera_prepass_kernel, rt_coherent.hip): samples in segments of one
+    // 8x8 tile x seg_frames (a power of two <= 64) frames, segment s = chunk * n_tiles + tile (chunk-major);
+    // the surface hits of segment s are records [s << seg_shift, + ccount[s]) of crec: (location.xyz, tag),
+    // tag = triangle | pixel-in-tile << 19 | frame-in-chunk << 25 | flipped normal << 31; the non-empty
+    // segments are listed in seg_list[0, *seg_list_n) (misses and light hits are parked by the pre-pass)
+    float4* crec; uint32_t* ccount; uint32_t* seg_list; uint32_t* seg_list_n;
+    uint32_t n_segments, n_tiles, seg_frames, seg_shift;
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray
@@ -81,6 +88,9 @@ int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t 
 // the vertex-synchronous kernel (rt_coherent.hip; no counters, no G-buffer): small scenes (n_lboxes > 0,
 // scene in LDS: LDS = scene | lane state) or, bvh = true, any scene in HBM (LDS = lane state)
 hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
+// its camera pre-pass: every sample's camera ray traced, misses / light hits parked, surface hits recorded
+// (KParams::crec); lds = the small scene's staged triangles + materials (0 for the BVH variant)
+hipError_t rt_launch_camera_prepass(const KParams& P, bool bvh, size_t lds, hipStream_t stream);
 int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes);
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)

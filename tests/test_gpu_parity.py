@@ -182,11 +182,12 @@ def test_exact_modes_agree_bitwise(ctx):
 
 
 def test_frame_chunks_are_bitwise_neutral(monkeypatch):
-    """Splitting a pixel's frames into work items (chunk 0 accumulates, later chunks park their samples
-    for the in-order finalize pass) leaves the accumulation bit-identical, from frame 1 and from a
-    later first frame."""
+    """Splitting a pixel's frames into work items (the megakernel: chunk 0 accumulates, later chunks park
+    their samples for the in-order finalize pass) leaves the accumulation bit-identical, from frame 1 and
+    from a later first frame."""
     W, H, spp = 40, 24, 37
     out = {}
+    monkeypatch.setenv("RT_VERTEX", "0")
     for chunks in ("1", "5", "37"):
         monkeypatch.setenv("RT_CHUNKS", chunks)
         c = rt.Context(0)
@@ -197,14 +198,35 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
             _, a = c.render(cam, 20, seed=3)
             _, b = c.render(cam, spp - 20, first_frame=21, seed=3)
             assert c.stats().n_chunks == min(int(chunks), spp - 20)
+            assert c.stats().kernel == 0   # the megakernel
             out[chunks] = (a, b)
         finally:
             c.close()
     for k in ("5", "37"):
         assert np.array_equal(bits(out[k][0]), bits(out["1"][0]))
         assert np.array_equal(bits(out[k][1]), bits(out["1"][1]))
-    # a parked-sample budget below one launch's needs splits the render into passes over frame ranges
+    monkeypatch.delenv("RT_VERTEX")
     monkeypatch.delenv("RT_CHUNKS")
+    # the vertex kernel: its camera pre-pass groups a tile's frames in segments of 64 (here 64 + 6)
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        _, v = c.render(cam, 70, seed=3)
+        assert c.stats().kernel == 1 and c.stats().n_chunks == 2
+    finally:
+        c.close()
+    monkeypatch.setenv("RT_VERTEX", "0")
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        _, m = c.render(cam, 70, seed=3)
+    finally:
+        c.close()
+    monkeypatch.delenv("RT_VERTEX")
+    assert np.array_equal(bits(v), bits(m))
+    # a parked-sample budget below one launch's needs splits the render into passes over frame ranges
     monkeypatch.setenv("RT_LBUF_BUDGET_MB", "1")
     c = rt.Context(0)
     try:
@@ -213,10 +235,9 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
         cam, _, _ = rt.camera_default(96, 64)
         _, a = c.render(cam, 100, seed=3)
         st = c.stats()
-        assert st.n_passes > 1 and st.n_chunks > 1
+        assert st.n_passes > 1
     finally:
         c.close()
-    monkeypatch.setenv("RT_CHUNKS", "1")
     monkeypatch.delenv("RT_LBUF_BUDGET_MB")
     c = rt.Context(0)
     try:
