@@ -744,7 +744,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             }
             if (want > 1 || park_all) {
                 // parked samples (12 B); the vertex kernel's camera records too (16 B)
-                const uint64_t bytes = px_local * (uint64_t)p->n_frames * (coh ? 28ull : 12ull);
+                const uint64_t bytes = px_local * (uint64_t)p->n_frames * (coh_box ? 28ull : 12ull);
                 passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
             }
             uint32_t done = 0;
@@ -777,8 +777,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
                 HIPC(c, hipMemsetAsync(c->d_counters + 3, 0, sizeof(unsigned long long), c->stream));   // this pass's overflow list
-                if (coh) {
-                    // segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
+                if (coh_box) {
+                    // the leaf-box variant's camera pre-pass: segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
                     uint32_t lf = 0;
                     while ((1u << lf) < nf && lf < 6) ++lf;
                     Q.seg_frames = 1u << lf;
@@ -804,7 +804,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     }
                     Q.crec = c->d_crec; Q.ccount = c->d_ccount; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
                     Q.n_chunks = (uint32_t)(nseg / Q.n_tiles);
-                    HIPC(c, rt_launch_camera_prepass(Q, coh_bvh, coh_bvh ? 0 : (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4), c->stream));
+                    HIPC(c, rt_launch_camera_prepass(Q, false, (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4), c->stream));
                 }
                 if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));

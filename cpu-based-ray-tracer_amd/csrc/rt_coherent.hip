@@ -100,6 +100,17 @@ struct VertexRng {
         fd.i = 0;
         dim += 6u;
     }
+    // the camera draws: dims 0 and 1 of block 0 (the block is kept in LDS only for unlit scenes, whose
+    // vertices draw through next())
+    __device__ __forceinline__ void camera_draws(uint32_t px, uint32_t fr, bool keep, float& ux, float& uy)
+    {
+        uint32_t o[4];
+        philox4x32_10(px, fr, 0u, 0u, k0, k1, o);
+        if (keep) { w[VS_RNG * 256u] = o[0]; w[(VS_RNG + 1) * 256u] = o[1]; w[(VS_RNG + 2) * 256u] = o[2]; w[(VS_RNG + 3) * 256u] = o[3]; }
+        ux = (float)o[0] / 4294967296.0f;
+        uy = (float)o[1] / 4294967296.0f;
+        dim = 2;
+    }
     // a new sample (pixel, frame) whose camera draws (dims 0 and 1, camera_prepass_kernel) are taken:
     // the vertices continue at dim 2; an unlit scene's vertices draw through next(), which finds dims 2
     // and 3 in the block kept in LDS
@@ -319,14 +330,21 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         complete(L, lsu(VS_DT0), lsu(VS_DT1));
     };
 
+    // PRE (the leaf-box variant): camera rays are traced by the pre-pass (camera_prepass_kernel) and a path
+    // starts here at its first surface vertex; the BVH variant traces its camera rays itself (a pre-pass
+    // cost it more than it saved, DESIGN.md 5.1: its time is in the secondary rays' BVH walks)
+    constexpr bool PRE = !BVH;
     bool alive = true, in_path = false;
+    bool have_pixel = false;   // !PRE: the lane holds a work item (frame chunk, pixel)
+    uint32_t k = 0;            // !PRE: frame of the current item (item of chunk c: frames c * chunk_frames + [0, kend))
+    bool pend = false;         // !PRE: the last vertex waits for its shadow verdict (false: the camera ray's hit)
+    uint32_t pool_base = 0, pool_count = 0;   // !PRE: the wave's batch of work items (wave-uniform)
     uint32_t depth = 0;   // vertices shaded so far on this path
     bool cont = false;    // the last vertex's roulette continued: ray A is its indirect ray
     VertexRng g;
     g.w = reinterpret_cast<uint32_t*>(lstate) + tib;
     g.k0 = (uint32_t)P.seed; g.k1 = (uint32_t)(P.seed >> 32);
-    // the lane's rays: A = indirect ray (closest hit), B = shadow ray (any hit); shared origin.  Camera rays
-    // are traced by the pre-pass (camera_prepass_kernel): a path starts here at its first surface vertex.
+    // the lane's rays: A = indirect (!PRE: or camera) ray (closest hit), B = shadow ray (any hit); shared origin
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
@@ -347,7 +365,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
     uint32_t seg_pos = 0, seg_end = 0;
-    const uint32_t n_list = __builtin_amdgcn_readfirstlane(*P.seg_list_n);
+    const uint32_t n_list = PRE ? __builtin_amdgcn_readfirstlane(*P.seg_list_n) : 0u;
     bool list_left = true;
 
 #if RT_SECTIONS
@@ -399,6 +417,59 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         if (need && rec == NO_REC) alive = false;
         return rec;
     };
+    // Lanes without a work item take the next ones from the wave's pool, in lane order.  With `refill`
+    // (the top of the iteration, before any store) an empty pool is refilled from the device counter;
+    // without it (after the path-end block, so a lane whose item just ended starts the next one's camera
+    // ray in the same iteration) only the pool's items are handed out -- no atomic, so nothing waits for
+    // the iteration's stores.  (!PRE)
+    auto take_items = [&](const bool refill) {
+        const bool need = alive && !have_pixel;
+        const uint64_t mask = __ballot(need);
+        if (mask == 0) return;
+        CKParams& Q = kargs4();
+        uint32_t n = (uint32_t)__popcll(mask);
+        if (!refill && n > pool_count) n = pool_count;
+        if (n == 0) return;
+        uint32_t fresh = 0;   // first item of a new batch (wave-uniform)
+        if (n > pool_count) {
+            uint32_t b = 0;
+            if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) b = atomicAdd(Q.work_counter, 64u);
+            fresh = __builtin_amdgcn_readfirstlane(b);
+        }
+        const uint32_t j = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (need && j < n) {
+            const uint32_t w = j < pool_count ? pool_base + j : fresh + (j - pool_count);
+            if (w >= Q.n_items) {
+                alive = false;
+            } else {
+                // item = (frame chunk, pixel), chunk-major; 8x8 tile swizzle in local (row, column) space
+                const uint32_t c = w / Q.items_per_chunk, wp = w - c * Q.items_per_chunk;
+                const uint32_t tile = wp >> 6, within = wp & 63u;
+                const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
+                const uint32_t lr = trow * 8u + (within >> 3), lx = tcol * 8u + (within & 7u);
+                if (lr < Q.n_local_rows && lx < Q.W) {
+                    // local row -> global row (row bands dealt round-robin over ranks)
+                    const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+                    const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
+                    const uint32_t local = lr * Q.W + lx;
+                    lsu(VS_LOCAL) = local;
+                    lsu(VS_PIX) = y * Q.W + lx;
+                    lsu(VS_FRAME) = Q.first_frame + c * Q.chunk_frames;   // the frame of the item's first sample
+                    have_pixel = true;
+                    k = 0;
+                }
+            }
+        }
+        // (64 items per refill: a wave's pool never holds more than one item per lane, so the launch
+        // tail stays one item long)
+        if (n > pool_count) {
+            pool_base = fresh + (n - pool_count);
+            pool_count = 64u - (n - pool_count);
+        } else {
+            pool_base += n;
+            pool_count -= n;
+        }
+    };
     for (;;) {
         SEC_MARK(0);
         // ======================= the lanes whose path ends in this iteration's service =======================
@@ -412,14 +483,20 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             mat = f2i(S.tris[4 * triA].w);
             emissive = S.mats[2 * mat].w != 0.0f;
         }
-        const bool ends = served && (!cont || triA < 0 || emissive);
-        const uint32_t rid = take_records(alive && (!in_path || ends));
+        const bool ends = served && (PRE || pend) && (!cont || triA < 0 || emissive);
+        uint32_t rid = NO_REC;
         float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (rid != NO_REC) rec = kargs4().crec[rid];
+        if constexpr (PRE) {
+            rid = take_records(alive && (!in_path || ends));
+            if (rid != NO_REC) rec = kargs4().crec[rid];
+        }
         if (EXACT && __any(dleft != 0u)) {
             if (dleft != 0u) drain_step(dleft);
         }
         SEC_MARK(3);
+        // !PRE: at the top of the iteration, before any store, a lane that finished its item takes the next
+        // one (the returning atomic waits for no store of this iteration)
+        if constexpr (!PRE) take_items(true);
 
         // ======================= service: the lanes whose rays are back =======================
         bool vertex = false;   // a surface vertex to shade: the indirect ray's hit, or a new path's camera hit
@@ -429,67 +506,81 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
             bool relisted = false;   // EXACT: the sample went to the overflow list (no fold, no parked store)
             V3 L{0.f, 0.f, 0.f};
-            // the last vertex's direct term (MC/Renderer.cpp:184-189): the shadow verdict
-            V3 ld{0.f, 0.f, 0.f};
-            if (hasB && !occB) ld = ls3(VS_LD);
-            if (!EXACT) {
-                const V3 thr = ls3(VS_THR);
-                const V3 lsum = add(ls3(VS_LSUM), mul(thr, ld));
-                if (ends) {
-                    L = lsum;
+            if (!PRE && !pend) {
+                // the camera ray's hit (cast_path, MC/Renderer.cpp:136-146)
+                if (triA < 0) {   // miss: night sky (:145)
+                    L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
+                    finished = true;
+                } else if (emissive) {   // direct emission (:151-161)
+                    const float4 em = S.mats[2 * mat + 1];
+                    L = V3{em.x, em.y, em.z};
                     finished = true;
                 } else {
-                    st3(VS_LSUM, lsum);
-                    const float c = lsf(VS_PCOS);
-                    const float4 mb = S.mats[2 * lsu(VS_MAT)];
-                    const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                    st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
                     vertex = true;
                 }
-            } else if (ends) {
-                L = ld;
-                fold_top = (int)depth - 2;
-                finished = true;
             } else {
-                // the indirect ray hit a surface: vertex depth-1 becomes stack level depth-1
-                const uint32_t lvl = depth - 1;
-                const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
-                const uint32_t pm = lsu(VS_MAT);
-                const uint32_t R = Q.stack_depth;
-                uint32_t pos = lsu(VS_BASE) + lvl;
-                if (pos >= R) pos -= R;
-                // the ring holds this path's levels above the draining ones, which occupy the R positions
-                // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
-                bool fits = lvl < R;
-                if (fits && dleft != 0u) {
-                    const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
-                    fits = (pos + R - lo) % R >= dleft;
-                }
-                if (fits) {
-                    if (Q.ring_pack) {
-                        // the material in the sign bits of the direct term (rt_kernels.h ring_pack)
-                        const float4 pe = make_float4(__uint_as_float((__float_as_uint(e.x) & 0x7FFFFFFFu) | ((pm & 1u) << 31)),
-                                                      __uint_as_float((__float_as_uint(e.y) & 0x7FFFFFFFu) | ((pm & 2u) << 30)),
-                                                      __uint_as_float((__float_as_uint(e.z) & 0x7FFFFFFFu) | ((pm & 4u) << 29)), e.w);
-                        Q.stack_ld[RING_AT(pos)] = pe;
+                // the last vertex's direct term (MC/Renderer.cpp:184-189): the shadow verdict
+                V3 ld{0.f, 0.f, 0.f};
+                if (hasB && !occB) ld = ls3(VS_LD);
+                if (!EXACT) {
+                    const V3 thr = ls3(VS_THR);
+                    const V3 lsum = add(ls3(VS_LSUM), mul(thr, ld));
+                    if (ends) {
+                        L = lsum;
+                        finished = true;
                     } else {
-                        Q.stack_ld[RING_AT(pos)] = e;
-                        Q.stack_mat[RING_AT(pos)] = pm;
+                        st3(VS_LSUM, lsum);
+                        const float c = lsf(VS_PCOS);
+                        const float4 mb = S.mats[2 * lsu(VS_MAT)];
+                        const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
+                        st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
+                        vertex = true;
                     }
-                    vertex = true;
-                } else {
-                    // the path outgrew the ring: list the sample for the exact re-render
-                    // (rt_resample.hip) and end it here; its parked slot is written there
-                    const uint32_t slot = (uint32_t)atomicAdd((unsigned long long*)&Q.counters[3], 1ull);
-                    const uint32_t frame = lsu(VS_FRAME);
-                    if (slot < Q.ovf_cap) {
-                        Q.ovf_list[slot] = make_uint4(lsu(VS_LOCAL), frame - Q.first_frame, lsu(VS_PIX), frame);
-                        atomicAdd((unsigned long long*)&Q.counters[14], 1ull);
-                    } else {
-                        atomicAdd((unsigned long long*)&Q.counters[13], 1ull);   // lost: rt_render reports it
-                    }
+                } else if (ends) {
+                    L = ld;
+                    fold_top = (int)depth - 2;
                     finished = true;
-                    relisted = true;
+                } else {
+                    // the indirect ray hit a surface: vertex depth-1 becomes stack level depth-1
+                    const uint32_t lvl = depth - 1;
+                    const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
+                    const uint32_t pm = lsu(VS_MAT);
+                    const uint32_t R = Q.stack_depth;
+                    uint32_t pos = lsu(VS_BASE) + lvl;
+                    if (pos >= R) pos -= R;
+                    // the ring holds this path's levels above the draining ones, which occupy the R positions
+                    // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
+                    bool fits = lvl < R;
+                    if (fits && dleft != 0u) {
+                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
+                        fits = (pos + R - lo) % R >= dleft;
+                    }
+                    if (fits) {
+                        if (Q.ring_pack) {
+                            // the material in the sign bits of the direct term (rt_kernels.h ring_pack)
+                            const float4 pe = make_float4(__uint_as_float((__float_as_uint(e.x) & 0x7FFFFFFFu) | ((pm & 1u) << 31)),
+                                                          __uint_as_float((__float_as_uint(e.y) & 0x7FFFFFFFu) | ((pm & 2u) << 30)),
+                                                          __uint_as_float((__float_as_uint(e.z) & 0x7FFFFFFFu) | ((pm & 4u) << 29)), e.w);
+                            Q.stack_ld[RING_AT(pos)] = pe;
+                        } else {
+                            Q.stack_ld[RING_AT(pos)] = e;
+                            Q.stack_mat[RING_AT(pos)] = pm;
+                        }
+                        vertex = true;
+                    } else {
+                        // the path outgrew the ring: list the sample for the exact re-render
+                        // (rt_resample.hip) and end it here; its parked slot is written there
+                        const uint32_t slot = (uint32_t)atomicAdd((unsigned long long*)&Q.counters[3], 1ull);
+                        const uint32_t frame = lsu(VS_FRAME);
+                        if (slot < Q.ovf_cap) {
+                            Q.ovf_list[slot] = make_uint4(lsu(VS_LOCAL), frame - Q.first_frame, lsu(VS_PIX), frame);
+                            atomicAdd((unsigned long long*)&Q.counters[14], 1ull);
+                        } else {
+                            atomicAdd((unsigned long long*)&Q.counters[13], 1ull);   // lost: rt_render reports it
+                        }
+                        finished = true;
+                        relisted = true;
+                    }
                 }
             }
             SEC_MARK(1);
@@ -499,8 +590,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             if (finished) {
                 in_path = false;
                 hasA = hasB = false;
-                const uint32_t local = lsu(VS_LOCAL);
-                const uint32_t fidx = lsu(VS_FRAME) - Q.first_frame;   // the sample's frame index in this launch
+                const uint32_t local = lsu(VS_LOCAL), frame = lsu(VS_FRAME);
+                const uint32_t fidx = frame - Q.first_frame;   // the sample's frame index in this launch
+                if (!PRE) {   // the item's next frame, or the end of the item
+                    const uint32_t kbase = fidx - k;   // the item's first frame index
+                    ++k;
+                    lsu(VS_FRAME) = frame + 1u;
+                    if (k == min(Q.chunk_frames, Q.n_frames - kbase)) have_pixel = false;
+                }
                 if (EXACT && relisted) {
                     // nothing to fold or park: resample_kernel writes this sample's slot
                 } else if (EXACT) {
@@ -531,13 +628,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 }
             }
         }
+        if constexpr (!PRE) take_items(false);
         SEC_MARK(4);
 
         // ======================= the vertex to shade: (location, triangle, face-forward) =======================
         V3 loc;
         int tri;
         bool flip;
-        if (rid != NO_REC) {
+        if (PRE && rid != NO_REC) {
             // a new path from its camera-hit record: sample (pixel, frame) from the segment and the tag
             // (rt_kernels.h crec), the location and face-forwarded normal as the pre-pass computed them
             CKParams& Q = kargs4();
@@ -630,6 +728,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
             hasA = cont;
             o = p;
+            pend = true;
             depth = depth + 1;
             if (BVH) {
                 tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
@@ -637,7 +736,38 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
         }
 
-        if (!__any(in_path || alive)) {
+        // ======================= !PRE, a new sample: camera ray (MC/Camera.cpp:119-125 + MC/Renderer.cpp:128)
+        if (!PRE && have_pixel && !in_path) {
+            CKParams& Q = kargs4();
+            const uint32_t pix = lsu(VS_PIX), y = pix / Q.W, x = pix - y * Q.W;
+            float ux, uy;
+            g.camera_draws(pix, lsu(VS_FRAME), !Q.has_light, ux, uy);
+#if RT_SECTIONS
+            dbg_cam = true;
+#endif
+            float cx = sdiv((float)x + ux, (float)Q.W, Q.y_w);
+            float cy = sdiv((float)y + uy, (float)Q.H, Q.y_h);
+            cx = cx * 2.0f - 1.0f;
+            cy = cy * 2.0f - 1.0f;
+            float tg[4];
+            mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
+            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
+            float wd[4];
+            mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
+            o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
+            dA = w_normalize(V3{wd[0], wd[1], wd[2]});
+            hasA = true; hasB = false;
+            depth = 0;
+            pend = false;
+            in_path = true;
+            if (BVH) {
+                tiA = 0u; tiB = NN;
+                tA = 1.7976931348623157e308; triA = -1; occB = false;
+            }
+            if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
+        }
+
+        if (!__any(in_path || alive || have_pixel)) {
             if (EXACT) drain_all(dleft);
             break;
         }
