@@ -4,14 +4,16 @@
 Workload (one "step"): the C4 configuration -- the reference's Cornell box at 1920x1080, 1024 spp
 (one sample = one camera path of one pixel in one frame, MC/Renderer.cpp:91-134), accumulated from
 frame 1, packed to RGBA8 and gathered to rank 0.  The image is dealt to the N ranks in 8-row bands
-(round-robin); each rank renders its bands in one persistent megakernel launch; RCCL all-gathers the
-RGBA8 bands (the only collective).  Total work is fixed as N grows ("scaling": "strong").
+(round-robin); each rank renders its bands (a camera pre-pass and the persistent vertex kernel per
+launch); RCCL all-gathers the RGBA8 bands (the only collective).  Total work is fixed as N grows
+("scaling": "strong").
 
     python bench.py                       # N=1, defaults finish in about a minute
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
-Prints ONE JSON line on rank 0 (value = whole-job Msamples/s), with the roofline of the megakernel
-(HIP events on the kernel's own stream) and the reference CPU baseline timed on this host.
+Prints ONE JSON line on rank 0 (value = whole-job Msamples/s), with the roofline of the path's kernels
+(HIP events on their own stream), a labelled FAST-mode rate (the cost of the exact fold) and the
+reference CPU baseline timed on this host.
 """
 import argparse
 import json
@@ -31,12 +33,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 # Moller-Trumbore tests per ray, shading calls.  Priced per SURVEY 8(d): node = 32 B / 18 flop, triangle
 # = 36 B / 54 flop (fp32-equivalent, incl. the fp64 part), shading = 16 B fetch / 150 flop.
 REF_WORK = {"rays_per_sample": 3.6475, "node_tests_per_ray": 24.619, "tri_tests_per_ray": 3.574, "shading_calls_per_sample": 1.4723}
-BYTES_PER_SAMPLE = REF_WORK["rays_per_sample"] * (REF_WORK["node_tests_per_ray"] * 32 + REF_WORK["tri_tests_per_ray"] * 36 + 16)
 FLOPS_PER_SAMPLE = (REF_WORK["rays_per_sample"] * (REF_WORK["node_tests_per_ray"] * 18 + REF_WORK["tri_tests_per_ray"] * 54)
                     + REF_WORK["shading_calls_per_sample"] * 150)
-# MI355X_MICROARCH.md / SURVEY.md 8(d): FP32 vector peak (dense, packed-FMA issue) and HBM3E peak
+# MI355X_MICROARCH.md / SURVEY.md 8(d): FP32 vector peak (dense, packed-FMA issue)
 VALU_PEAK_TFLOPS = 157.3
-HBM_PEAK_GBS = 8000.0
 # VALU issue peak: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md),
 # 256 CUs x 4 SIMDs at 2.4 GHz
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
@@ -188,8 +188,13 @@ def main():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--band", type=int, default=8)
     ap.add_argument("--fast", action="store_true", help="forward accumulation instead of the exact inner-first fold")
+    ap.add_argument("--no-fast-probe", action="store_true", help="skip the labelled FAST-mode rate (one extra render)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: RCCL on device tensors (the product path) or gloo on host-staged bands (tests: "
+                         "several ranks on one GPU, where RCCL needs one GPU per rank)")
+    ap.add_argument("--dump-image", default=None, help="rank 0 saves the gathered RGBA8 frame (.npy, row 0 = bottom)")
     args = ap.parse_args()
 
     import torch
@@ -198,14 +203,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = world > 1 and args.dist_backend == "gloo"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one GPU per rank (RCCL); with gloo several ranks may share a GPU
+        torch.cuda.set_device(local % torch.cuda.device_count() if gloo else local)
+        dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    # a dedicated (non-null) stream shared by the megakernel, the copies, RCCL and the torch ops,
-    # so every step is ordered on ONE stream and torch.cuda.Event sees the kernel
+    # a dedicated (non-null) stream shared by the kernels, the copies, RCCL and the torch ops, so every
+    # step is ordered on ONE stream and torch.cuda.Event sees the kernels
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     assert stream.cuda_stream != 0
@@ -219,70 +226,85 @@ def main():
     cam, _, _ = rt.camera_default(W, H)
 
     rtdist = load_dist()
-    gat = rtdist.ImageGather(W, H, args.band, rank, world, dev)
+    gat = rtdist.ImageGather(W, H, args.band, rank, world, torch.device("cpu") if gloo else dev)
+    stage = torch.zeros(gat.max_rows * W, dtype=torch.int32, device=dev) if gloo else None
     assert gat.n_local == ctx.local_rows
-    kernel_ms = []
+    kernel_ms, main_ms, pre_ms = [], [], []
     launch_info = {}
 
     def step():
         ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not args.fast, fetch=False)
-        ctx.copy_rgba_to_device(gat.send.data_ptr())   # this rank's rows, on the shared stream
-        gat.gather()                                    # RCCL all-gather + reassembly on rank 0
+        if gloo:   # host-staged bands: the device rows, then the gloo all-gather of host tensors
+            ctx.copy_rgba_to_device(stage.data_ptr())
+            gat.send.copy_(stage.cpu())
+        else:
+            ctx.copy_rgba_to_device(gat.send.data_ptr())   # this rank's rows, on the shared stream
+        gat.gather()                                        # all-gather + reassembly on rank 0
         st = ctx.stats()
         kernel_ms.append(st.last_kernel_ms)
+        main_ms.append(st.last_main_ms)
+        pre_ms.append(st.last_prepass_ms)
         launch_info.update(passes=st.n_passes, chunks=st.n_chunks, kernel=rt.KERNEL_NAMES.get(st.kernel, str(st.kernel)))
 
     for _ in range(args.warmup):
         step()
-    kernel_ms.clear()
+    kernel_ms.clear(); main_ms.clear(); pre_ms.clear()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record(stream)
     for _ in range(args.steps):
         step()
-    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
+        if gloo:
+            parts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, t)
+            per_rank = [float(x.item()) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
+    if args.dump_image and rank == 0:
+        np.save(args.dump_image, gat.image.cpu().numpy().view(np.uint32).reshape(H, W))
 
-    # roofline of the path-tracing kernel on this rank.  SURVEY.md 8(d): there is no dense contraction
-    # and the Cornell scene lives on chip, so the binding roof for C2/C4 is the vector ALU; the sample is
-    # priced by the REFERENCE's work (FLOPS_PER_SAMPLE), whatever the kernel prunes.  achieved = flops per
-    # launch / the kernel's mean launch time (HIP events on the kernel's stream, rt_stats.last_kernel_ms;
-    # a step is `passes` launches over consecutive frame ranges, each with its in-order finalize).
+    # Roofline of the path's kernels on this rank.  SURVEY.md 8(d): there is no dense contraction and the
+    # Cornell scene lives on chip, so the binding roof for C2/C4 is the vector ALU; the sample is priced by
+    # the REFERENCE's work (FLOPS_PER_SAMPLE), whatever the kernels prune.  The path runs as two kernels per
+    # launch (pass): camera_prepass_kernel traces the camera rays and parks the sky / light samples,
+    # pt_coherent_kernel renders every path from its first surface vertex.  achieved = flops per launch /
+    # (their mean per-launch time), each kernel timed with HIP events on the stream it runs on
+    # (rt_stats.last_prepass_ms / last_main_ms).
     local_samples = gat.n_local * W * spp
     passes = max(1, int(launch_info.get("passes", 1)))
-    k_s = float(np.mean(kernel_ms)) / 1e3 / passes if kernel_ms else float("nan")
+    main_s = float(np.mean(main_ms)) / 1e3 / passes if main_ms else float("nan")
+    pre_s = float(np.mean(pre_ms)) / 1e3 / passes if pre_ms else 0.0
+    k_s = main_s + pre_s
     per_launch = local_samples / passes
     tflops = FLOPS_PER_SAMPLE * per_launch / k_s / 1e12
-    alg_gbs = BYTES_PER_SAMPLE * per_launch / k_s / 1e9
     kname = launch_info.get("kernel", "?")
     digest = lib_digest(os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so"))
     pmc = counter_pass(kname, W, H, spp, not args.fast, world, passes, digest)
+    kernels = {kname: round(main_s * 1e3, 3)}
+    if pre_s > 0:
+        kernels["camera_prepass_kernel"] = round(pre_s * 1e3, 3)
     roof = {"bound": "valu", "achieved": round(tflops, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tflops / VALU_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": kname, "kernel_ms": round(k_s * 1e3, 3), "flops_per_sample": round(FLOPS_PER_SAMPLE, 1),
+            "kernel": " + ".join(kernels), "kernel_ms": round(k_s * 1e3, 3), "kernel_ms_each": kernels,
+            "dominant_kernel": kname, "dominant_frac_of_time": round(main_s / k_s, 4),
+            "render_ms_with_finalize": round(float(np.mean(kernel_ms)), 3) if kernel_ms else None,
+            "flops_per_sample": round(FLOPS_PER_SAMPLE, 1),
             "samples_per_launch": int(per_launch), "launches_per_step": passes,
-            "frame_chunks": int(launch_info.get("chunks", 1)), "gsamples_per_s_kernel": round(per_launch / k_s / 1e9, 4),
-            "reference_work": REF_WORK,
-            # secondary, labelled: the reference's algorithmic bytes against HBM.  > 1 is possible and means
-            # HBM is not the binding roof -- those bytes are LDS / scalar-cache reads of an on-chip scene
-            "hbm_algorithmic": {"bytes_per_sample": round(BYTES_PER_SAMPLE, 1), "achieved_gbs": round(alg_gbs, 1),
-                                "peak_gbs": HBM_PEAK_GBS, "frac": round(alg_gbs / HBM_PEAK_GBS, 4)},
-            "lib_sha256": digest, "counters": None}
+            "frame_chunks": int(launch_info.get("chunks", 1)), "gsamples_per_s_kernels": round(per_launch / k_s / 1e9, 4),
+            "reference_work": REF_WORK, "lib_sha256": digest, "counters": None}
     if pmc is not None:
         # a rocprofv3 counter pass of this build and shape (profiles/): HBM bytes per launch and the
-        # kernel's VALU issue fraction / lane utilization
+        # kernels' VALU issue fraction / lane utilization
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
         roof["counters"] = {"file": pmc["_file"], "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
                             "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
@@ -290,6 +312,18 @@ def main():
                             "kernel_ms_profiled": pmc.get("kernel_ms"), "traffic_method": pmc.get("hbm_correction"),
                             "read_bytes_per_sample": pmc.get("split_read_bytes_per_sample"),
                             "write_bytes_per_sample": pmc.get("split_write_bytes_per_sample")}
+
+    # labelled secondary: the FAST mode's rate on this rank (forward throughput accumulation: within RMSE 1e-5
+    # of the reference, not its rounding sequence) -- what the EXACT inner-first fold (MC/Renderer.cpp:208,213)
+    # costs; one render after the timed steps, kernels only
+    fast = None
+    if not args.fast and not args.no_fast_probe:
+        ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=False, fetch=False)
+        st = ctx.stats()
+        fk = (st.last_main_ms + st.last_prepass_ms) / 1e3
+        fast = {"msamples_per_s_kernels_rank": round(local_samples / fk / 1e6, 1), "kernel_ms": round(fk * 1e3, 3),
+                "exact_msamples_per_s_kernels_rank": round(local_samples / (k_s * passes) / 1e6, 1),
+                "exact_cost": round(k_s * passes / fk - 1.0, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -306,8 +340,10 @@ def main():
             "vs_baseline": None, "dtype": "f32+f64", "data": "synthetic (reference Cornell box scene, Philox RNG seed 0)",
             "config": {"workload": f"C4 cornell {W}x{H} {spp}spp", "width": W, "height": H, "spp": spp, "rr": 0.8,
                        "seed": 0, "band_rows": args.band, "accumulation": "fast" if args.fast else "exact",
-                       "parallelism": f"row-bands x{world}"},
+                       "parallelism": f"row-bands x{world}", "dist_backend": args.dist_backend if world > 1 else None},
             "roofline": roof,
+            "fast_mode": fast,
+            "rank_elapsed_s": [round(x, 6) for x in per_rank],
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -51,13 +51,13 @@ class Stats(C.Structure):
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
                 ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
                 ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64),
-                ("pair_cap", C.c_uint32)]
+                ("pair_cap", C.c_uint32), ("last_prepass_ms", C.c_float), ("last_main_ms", C.c_float)]
 
 class GroupStats(C.Structure):
     _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
 
 
-_DIAGNOSTIC = {"rt_debug_counters"}
+_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation"}   # may be absent from an older A/B build
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 
@@ -81,7 +81,7 @@ REFLECTIVE, REFLECTIVE_REFRACTIVE, DIFFUSE_GLOSSY = 0, 1, 2
 class SceneInfo(C.Structure):
     _fields_ = [("n_meshes", C.c_uint32), ("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_light_tris", C.c_uint32),
                 ("max_depth", C.c_uint32), ("light_mesh", C.c_int32), ("light_area", C.c_float), ("device_bytes", C.c_uint64),
-                ("n_leaf_boxes", C.c_uint32)]
+                ("n_leaf_boxes", C.c_uint32), ("n_light_skip", C.c_uint32)]
 
 
 def _fp(a):
@@ -126,6 +126,7 @@ def lib():
         "rt_render": (i32, [vp, C.POINTER(Camera), C.POINTER(RenderParams), C.POINTER(u32), fp]),
         "rt_device_buffers": (i32, [vp, C.POINTER(vp), C.POINTER(vp)]),
         "rt_copy_rgba_to_device": (i32, [vp, vp]),
+        "rt_read_accumulation": (i32, [vp, C.POINTER(C.c_float)]),
         "rt_reset_accumulation": (i32, [vp]),
         "rt_synchronize": (i32, [vp]),
         "rt_get_stats": (i32, [vp, C.POINTER(Stats)]),
@@ -546,6 +547,13 @@ class Context:
         a, r = C.c_void_p(), C.c_void_p()
         self._check(lib().rt_device_buffers(self.h, C.byref(a), C.byref(r)), "rt_device_buffers")
         return a.value, r.value
+
+    def accumulation(self):
+        """The local float4 accumulation after a synchronisation (rt_read_accumulation; RtError on an EXACT
+        overflow of the renders since the last check)."""
+        a = np.zeros((self.local_rows, self.W, 4), np.float32)
+        self._check(lib().rt_read_accumulation(self.h, _fp(a)), "rt_read_accumulation")
+        return a
 
     def copy_rgba_to_device(self, dst_ptr):
         self._check(lib().rt_copy_rgba_to_device(self.h, C.c_void_p(dst_ptr)), "rt_copy_rgba_to_device")

@@ -68,6 +68,10 @@ struct rt_ctx {
     uint32_t n_cu = 0;
     int occ_global[2][2] = {{0, 0}, {0, 0}};              // blocks per CU, [exact][count], scene in HBM
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // per pass: events before the camera pre-pass, between it and the path kernel, after the path kernel
+    std::vector<hipEvent_t> kev;
+    uint32_t kev_used = 0;        // passes of the last render with kernel events
+    bool kev_prepass = false;     // the last render ran the camera pre-pass
     rt_stats stats{};
     bool pending_stats = false;
     uint32_t last_flags = 0;
@@ -151,8 +155,16 @@ rt_status check_overflow(rt_ctx* c)
 {
     if (!c->pending_check) return RT_OK;
     c->pending_check = false;
+    // h_ovf holds the device totals since the last check (the last render's copy, after the stream
+    // synchronised); they are cleared for the next renders
     c->stats.overflow_lost = c->h_ovf[0];
     c->stats.resampled = c->h_ovf[1];
+    if (c->h_ovf[0] != 0 || c->h_ovf[1] != 0) {
+        if (hipMemsetAsync(c->d_counters + 13, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess) {
+            c->err = "clearing the overflow counters failed";
+            return RT_ERR_HIP;
+        }
+    }
     if (c->h_ovf[0] != 0) {
         c->err = "EXACT fold stack overflow: " + std::to_string(c->h_ovf[0]) + " path level(s) or sample(s) lost (stack depth " +
                  std::to_string(c->stack_depth) + ", rr too close to 1 for the megakernel's stack)";
@@ -356,6 +368,13 @@ rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
     info->device_bytes = (s->flat.nodes.size() + s->flat.tris.size() + s->flat.mats.size() + s->flat.lnodes.size() + s->flat.ltris.size() +
                           s->flat.lboxes.size()) * 4;
     info->n_leaf_boxes = h.n_lboxes;
+    uint32_t skip = 0;   // the light triangles' candidate-skip masks (rt_layout.h ltris word 3)
+    for (size_t k = 0; k + 15 < s->flat.ltris.size(); k += 16) {
+        uint32_t m;
+        std::memcpy(&m, &s->flat.ltris[k + 3], 4);
+        skip += (uint32_t)__builtin_popcount(m);
+    }
+    info->n_light_skip = skip;
     return RT_OK;
 }
 
@@ -416,6 +435,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
         rt_destroy(c);
         return RT_ERR_HIP;
     }
+    if (hipMemset(c->d_counters, 0, kCounterWords * 8) != hipSuccess) { c->err = "hipMemset failed"; rt_destroy(c); return RT_ERR_HIP; }
     // persistent grid: every CU filled to the kernel's occupancy
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->device) != hipSuccess) { c->err = "hipGetDeviceProperties failed"; rt_destroy(c); return RT_ERR_HIP; }
@@ -456,6 +476,7 @@ void rt_destroy(rt_ctx* c)
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
     dfree(c->d_ovf); dfree(c->d_rs_stack); dfree(c->d_rs_mat);
     if (c->h_ovf) (void)hipHostFree(c->h_ovf);
+    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -526,19 +547,31 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     const uint32_t n = s->flat.hdr.n_tris, m = 2 * n - 1;
     float* d_verts = nullptr;
     float4 *d_nodes = nullptr, *d_tris = nullptr;
-    auto fail = [&](hipError_t e) { dfree(d_verts); dfree(d_nodes); dfree(d_tris); return hip_fail(c, e, "rt_upload_scene_gpu_bvh"); };
+    // the build is timed with its own events: the context's ev0/ev1 time renders, whose pending stats
+    // (rt_get_stats) must not pick up the build's time
+    hipEvent_t b0 = nullptr, b1 = nullptr;
+    auto fail = [&](hipError_t e) {
+        dfree(d_verts); dfree(d_nodes); dfree(d_tris);
+        if (b0) (void)hipEventDestroy(b0);
+        if (b1) (void)hipEventDestroy(b1);
+        return hip_fail(c, e, "rt_upload_scene_gpu_bvh");
+    };
     hipError_t e;
+    if ((e = hipEventCreate(&b0)) != hipSuccess) return fail(e);
+    if ((e = hipEventCreate(&b1)) != hipSuccess) return fail(e);
     if ((e = hipMalloc((void**)&d_verts, verts.size() * sizeof(float))) != hipSuccess) return fail(e);
     if ((e = hipMalloc((void**)&d_nodes, 2 * (size_t)m * sizeof(float4))) != hipSuccess) return fail(e);
     if ((e = hipMalloc((void**)&d_tris, 4 * (size_t)n * sizeof(float4))) != hipSuccess) return fail(e);
     if ((e = hipMemcpy(d_verts, verts.data(), verts.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) return fail(e);
-    if ((e = hipEventRecord(c->ev0, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipEventRecord(b0, c->stream)) != hipSuccess) return fail(e);
     if ((e = lbvh_build_device(n, d_verts, c->d_tris, d_nodes, d_tris, c->stream)) != hipSuccess) return fail(e);
-    if ((e = hipEventRecord(c->ev1, c->stream)) != hipSuccess) return fail(e);
-    if ((e = hipEventSynchronize(c->ev1)) != hipSuccess) return fail(e);
+    if ((e = hipEventRecord(b1, c->stream)) != hipSuccess) return fail(e);
+    if ((e = hipEventSynchronize(b1)) != hipSuccess) return fail(e);
     float ms = 0.0f;
-    (void)hipEventElapsedTime(&ms, c->ev0, c->ev1);
+    (void)hipEventElapsedTime(&ms, b0, b1);
     if (build_ms) *build_ms = ms;
+    (void)hipEventDestroy(b0);
+    (void)hipEventDestroy(b1);
     dfree(d_verts);
     dfree(c->d_nodes); dfree(c->d_tris);
     c->d_nodes = d_nodes; c->d_tris = d_tris;
@@ -708,7 +741,13 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const uint64_t px_local = (uint64_t)c->local_rows * c->W;
     const uint64_t items_px = P.n_items;   // 8x8-tile-padded pixel items
     c->last_flags = p->flags;
-    HIPC(c, hipMemsetAsync(c->d_counters, 0, kCounterWords * 8, c->stream));
+    // (counters[13..14], the EXACT overflow outcome, are not reset here: they accumulate over renders
+    // until a synchronisation point reads them (check_overflow), so an earlier asynchronous render's loss
+    // is never masked by a later clean one)
+    HIPC(c, hipMemsetAsync(c->d_counters, 0, 13 * 8, c->stream));
+    HIPC(c, hipMemsetAsync(c->d_counters + 15, 0, (kCounterWords - 15) * 8, c->stream));
+    c->kev_used = 0;
+    c->kev_prepass = false;
     if (p->n_frames > 0 && c->local_rows > 0) {
         HIPC(c, hipEventRecord(c->ev0, c->stream));
         if (whitted && c->hdr.n_went > 0) {
@@ -777,6 +816,12 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 }
                 HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
                 HIPC(c, hipMemsetAsync(c->d_counters + 3, 0, sizeof(unsigned long long), c->stream));   // this pass's overflow list
+                while (c->kev.size() < 3 * (size_t)(pass + 1)) {
+                    hipEvent_t e = nullptr;
+                    HIPC(c, hipEventCreate(&e));
+                    c->kev.push_back(e);
+                }
+                HIPC(c, hipEventRecord(c->kev[3 * pass], c->stream));
                 if (coh_box) {
                     // the leaf-box variant's camera pre-pass: segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
                     uint32_t lf = 0;
@@ -806,8 +851,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.n_chunks = (uint32_t)(nseg / Q.n_tiles);
                     HIPC(c, rt_launch_camera_prepass(Q, false, (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4), c->stream));
                 }
+                HIPC(c, hipEventRecord(c->kev[3 * pass + 1], c->stream));
                 if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
+                HIPC(c, hipEventRecord(c->kev[3 * pass + 2], c->stream));
                 // EXACT vertex kernel: the samples whose path outgrew the ring, rendered again into their
                 // parked slots (exits at once when none was listed)
                 if (coh && exact) HIPC(c, rt_launch_resample(Q, c->rs_threads, c->stream));
@@ -816,6 +863,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 done += nf;
             }
             c->stats.n_passes = passes;
+            c->kev_used = passes;
+            c->kev_prepass = coh_box;
         }
         c->stats.grid = grid;
         c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh_bvh ? RT_KERNEL_VERTEX_BVH : coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);
@@ -942,6 +991,17 @@ rt_status rt_device_buffers(rt_ctx* c, void** d_accum, void** d_rgba)
     return RT_OK;
 }
 
+rt_status rt_read_accumulation(rt_ctx* c, float* out_accum)
+{
+    if (!c || !out_accum) return RT_ERR_INVALID;
+    if (!c->d_accum) { c->err = "no viewport (rt_resize)"; return RT_ERR_STATE; }
+    HIPC(c, hipSetDevice(c->device));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const rt_status ov = check_overflow(c);
+    if (c->local_rows > 0) HIPC(c, hipMemcpy(out_accum, c->d_accum, (size_t)c->local_rows * c->W * 16, hipMemcpyDeviceToHost));
+    return ov;
+}
+
 rt_status rt_copy_rgba_to_device(rt_ctx* c, void* dst)
 {
     if (!c || !dst) return RT_ERR_INVALID;
@@ -979,9 +1039,18 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
         float ms = 0.0f;
         HIPC(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->stats.last_kernel_ms = ms;
+        float pre = 0.0f, main = 0.0f;
+        for (uint32_t i = 0; i < c->kev_used && 3 * (size_t)i + 2 < c->kev.size(); ++i) {
+            float a = 0.0f, b = 0.0f;
+            HIPC(c, hipEventElapsedTime(&a, c->kev[3 * i], c->kev[3 * i + 1]));
+            HIPC(c, hipEventElapsedTime(&b, c->kev[3 * i + 1], c->kev[3 * i + 2]));
+            pre += a; main += b;
+        }
+        c->stats.last_prepass_ms = c->kev_prepass ? pre : 0.0f;
+        c->stats.last_main_ms = main;
         unsigned long long h[16] = {};   // [3]: the last pass's overflow list; [13] lost, [14] listed in all passes
         HIPC(c, hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
-        c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2]; c->stats.stack_overflows = h[13] + h[14];
+        c->stats.node_tests = h[0]; c->stats.tri_tests = h[1]; c->stats.rays = h[2];
         c->stats.wave_rounds = h[4]; c->stats.wave_steps = h[5]; c->stats.wave_tri_tests = h[6]; c->stats.wave_service = h[7];
         c->stats.wave_fold = h[8]; c->stats.cycles_service = h[9]; c->stats.cycles_queue = h[10]; c->stats.cycles_trace = h[11];
         c->stats.service_lanes = h[12];
@@ -989,6 +1058,8 @@ rt_status rt_get_stats(rt_ctx* c, rt_stats* st)
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     const rt_status ov = check_overflow(c);
+    // the overflow outcome as of the last check (resampled + lost, summed since the check before it)
+    c->stats.stack_overflows = c->stats.resampled + c->stats.overflow_lost;
     if (c->pending_denoise) {
         HIPC(c, hipEventSynchronize(c->ev3));
         float ms = 0.0f;
@@ -1029,6 +1100,7 @@ rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, in
     }
     cleanup();
     c->pending_stats = true;   // last_kernel_ms = the trace kernel
+    c->kev_used = 0;
     return RT_OK;
 }
 

@@ -350,6 +350,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     float slen = 0.0f;                        // length(q - p) of the shadow ray
     uint32_t bskip = 0;                       // NARROW: shadow-ray candidates that cannot block (light plane)
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
+    V3 hloc{0.f, 0.f, 0.f};                   // !BVH: ray A's hit location (from the trace) ...
+    bool hflip = false;                       // ... and whether its normal faces away from -dA
     int triA = -1;                            // closest triangle
     bool occB = false;                        // shadow ray blocked
     // EXACT: a finished path's levels are folded DRAIN_STEP per iteration ("drain"), not in a loop at the
@@ -472,6 +474,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     };
     for (;;) {
         SEC_MARK(0);
+        // (the leaf-box variant's rays are set up and traced within an iteration: not loop-carried)
+        if constexpr (!BVH) { o = V3{0.f, 0.f, 0.f}; dA = o; dB = o; }
         // ======================= the lanes whose path ends in this iteration's service =======================
         // decided from the trace results before any store: the roulette stopped, or the indirect ray missed or
         // hit the light (radiance_indirect = 0, MC/Renderer.cpp:193-209).  They and the idle lanes take their
@@ -484,14 +488,15 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             emissive = S.mats[2 * mat].w != 0.0f;
         }
         const bool ends = served && (PRE || pend) && (!cont || triA < 0 || emissive);
+        if (EXACT && __any(dleft != 0u)) {
+            if (dleft != 0u) drain_step(dleft);
+        }
+        // (after the drain's ring loads are folded: the record's registers are then not live across them)
         uint32_t rid = NO_REC;
         float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (PRE) {
             rid = take_records(alive && (!in_path || ends));
             if (rid != NO_REC) rec = kargs4().crec[rid];
-        }
-        if (EXACT && __any(dleft != 0u)) {
-            if (dleft != 0u) drain_step(dleft);
         }
         SEC_MARK(3);
         // !PRE: at the top of the iteration, before any store, a lane that finished its item takes the next
@@ -666,11 +671,17 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             dbg_cam = true;
 #endif
         } else {
-            // the indirect ray's hit: Ray::operator() (MC/Ray.h:34-37) and the face-forward against -dA
+            // the traced hit (the indirect ray's, or !PRE the camera ray's): Ray::operator() (MC/Ray.h:34-37) and
+            // the face-forward against -dA
             tri = triA;
-            loc = add(o, smul((float)tA, dA));
-            const float4 tn = (BVH && kargs4().use_qnodes) ? kargs4().tnrm[tri < 0 ? 0 : tri] : S.tris[4 * (tri < 0 ? 0 : tri) + 3];
-            flip = dot(V3{tn.x, tn.y, tn.z}, neg(dA)) < 0.0f;
+            if (BVH) {
+                loc = add(o, smul((float)tA, dA));
+                const float4 tn = kargs4().use_qnodes ? kargs4().tnrm[tri < 0 ? 0 : tri] : S.tris[4 * (tri < 0 ? 0 : tri) + 3];
+                flip = dot(V3{tn.x, tn.y, tn.z}, neg(dA)) < 0.0f;
+            } else {
+                loc = hloc;
+                flip = hflip;
+            }
         }
 #if RT_SECTIONS
         dbg_vertex = vertex;
@@ -932,6 +943,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 else cb = cur & (cur - 1);
                 test(useA, tri, cb);
             }
+        }
+        // the hit's location (Ray::operator(), MC/Ray.h:34-37) and the face-forward of its normal against
+        // -dA (MC/Renderer.cpp:163-166), formed here: the next iteration's vertex needs only these, so the
+        // rays (o, dA, dB) and the double t are not live across the iteration boundary
+        if (trA && triA >= 0) {
+            hloc = add(o, smul((float)tA, dA));
+            const float4 tn = S.tris[4 * triA + 3];
+            hflip = dot(V3{tn.x, tn.y, tn.z}, neg(dA)) < 0.0f;
         }
 #if RT_SECTIONS >= 3
         {   // [320 + tri] ray A's closest hits by triangle, [352] blocked ray-B lanes (fin lanes)

@@ -270,10 +270,8 @@ rt_status rt_group_read_accumulation(rt_group* g, float* out_accum)
     for (uint32_t i = 0; i < n; ++i) {
         local.resize((size_t)g->rows[i] * W * 4);
         if (local.empty()) continue;
-        // an empty render (0 frames) copies the member's accumulation out after a synchronisation
-        const rt_render_params p0{1u, 0u, 0u, 0.5f, 0u};
-        const rt_camera cam{};
-        GMEM(g, i, rt_render(g->m[i], &cam, &p0, nullptr, local.data()));
+        // the member's accumulation after a synchronisation (its stats stay those of its last render)
+        GMEM(g, i, rt_read_accumulation(g->m[i], local.data()));
         for (uint32_t r = 0; r < g->rows[i]; ++r) {
             const uint32_t y = (i + (r / band) * n) * band + r % band;
             std::memcpy(out_accum + (size_t)y * W * 4, local.data() + (size_t)r * W * 4, (size_t)W * 4 * sizeof(float));

@@ -115,14 +115,17 @@ __host__ __device__ inline void write_node(float* nodes, uint32_t pos, const flo
 }
 
 // ------------------------------------------------------------------ device pipeline
+// float min / max on the ordered integer images: a float with the sign bit clear orders as a signed
+// int, one with the sign bit set in reverse as an unsigned int.  The branch is on the sign BIT: -0.0
+// (0x80000000) must take the unsigned path, where it orders above every negative float's image.
 __device__ inline void atomic_min_f(float* a, float v)
 {
-    if (v >= 0.0f) atomicMin((int*)a, __float_as_int(v));
+    if (__float_as_int(v) >= 0) atomicMin((int*)a, __float_as_int(v));
     else atomicMax((unsigned int*)a, __float_as_uint(v));
 }
 __device__ inline void atomic_max_f(float* a, float v)
 {
-    if (v >= 0.0f) atomicMax((int*)a, __float_as_int(v));
+    if (__float_as_int(v) >= 0) atomicMax((int*)a, __float_as_int(v));
     else atomicMin((unsigned int*)a, __float_as_uint(v));
 }
 __device__ inline float load_c(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }

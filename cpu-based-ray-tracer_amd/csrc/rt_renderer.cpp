@@ -8,6 +8,8 @@
 #include "rt_camera.h"
 #include "rt_scene.h"
 
+namespace rt {
+
 // ============================================================================ Camera
 Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance)
     : vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance}, far_clip_plane_distance{FarClipPlaneDistance}
@@ -145,6 +147,8 @@ const std::vector<rt::vec3>& Camera::RayDirections(uint32_t frame, uint64_t seed
     return ray_directions;
 }
 
+}  // namespace rt
+
 // ============================================================================ entities
 rt::TriangleMesh::TriangleMesh(const std::string& file_path, const Material& m) : material_(m)
 {
@@ -155,6 +159,8 @@ rt::TriangleMesh::TriangleMesh(const std::string& file_path, const Material& m) 
 rt::TriangleMesh::TriangleMesh(std::vector<float> raw_positions, const Material& m) : raw_(std::move(raw_positions)), material_(m) {}
 
 // ============================================================================ Renderer
+namespace rt {
+
 void Renderer::check(rt_status s, const char* what) const
 {
     if (s != RT_OK)
@@ -251,14 +257,9 @@ const std::vector<float>& Renderer::GetAccumulation()
         if (!accum_host.empty()) check(rt_group_read_accumulation(group, accum_host.data()), "rt_group_read_accumulation");
         return accum_host;
     }
-    void* d_acc = nullptr;
-    check(rt_device_buffers(ctx, &d_acc, nullptr), "rt_device_buffers");
     const size_t n = frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0;
     accum_host.resize(n);
-    // a render with a host pointer synchronises; this re-reads the device buffer
-    rt_render_params p{frame_accumulating, 0, settings.seed + epoch, RR_survival_probability, 0};
-    const rt_camera cam{};
-    check(rt_render(ctx, &cam, &p, nullptr, accum_host.data()), "read accumulation");
+    if (n) check(rt_read_accumulation(ctx, accum_host.data()), "rt_read_accumulation");
     return accum_host;
 }
 
@@ -273,6 +274,8 @@ float Renderer::LastKernelMilliseconds() const
     if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
     return st.last_kernel_ms;
 }
+
+}  // namespace rt
 
 // ============================================================================ WhittedRenderer
 #include "rt/WhittedRenderer.h"

@@ -32,8 +32,6 @@ struct CameraInput {   // what Walnut::Input provided (MC/Camera.cpp:32-80)
     float mouse_dx = 0, mouse_dy = 0;
 };
 
-}  // namespace rt
-
 class Camera {
 public:
     Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance);
@@ -77,5 +75,13 @@ private:
     float far_clip_plane_distance = 100.0f;
     mutable std::vector<rt::vec3> ray_directions;
 };
+
+}  // namespace rt
+
+// The reference's global name (MC/Camera.h:15).  A Walnut front-end includes rt/walnut/Camera.h instead,
+// whose global Camera speaks glm and Walnut::Input (it defines RT_NO_GLOBAL_NAMES).
+#ifndef RT_NO_GLOBAL_NAMES
+using Camera = rt::Camera;
+#endif
 
 #endif

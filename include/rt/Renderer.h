@@ -61,8 +61,6 @@ public:
     using std::runtime_error::runtime_error;
 };
 
-}  // namespace rt
-
 class Renderer {
 public:
     struct Settings {
@@ -110,5 +108,13 @@ private:
     std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
     bool bvh_dirty = true;
 };
+
+}  // namespace rt
+
+// The reference's global name (MC/Renderer.h:30).  A Walnut front-end includes rt/walnut/Renderer.h
+// instead, whose global Renderer hands Walnut::Image frames to the layer (it defines RT_NO_GLOBAL_NAMES).
+#ifndef RT_NO_GLOBAL_NAMES
+using Renderer = rt::Renderer;
+#endif
 
 #endif

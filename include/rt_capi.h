@@ -104,6 +104,8 @@ typedef struct {
     float light_area;
     uint64_t device_bytes; /* bytes the flattened scene occupies in HBM */
     uint32_t n_leaf_boxes; /* distinct leaf boxes of a small scene's coherent trace (0: BVH traversal) */
+    uint32_t n_light_skip; /* (light triangle, triangle) pairs whose shadow-ray candidates the vertex kernel skips
+                              (near-coplanar with the light; 0 when the scene's error bound does not hold) */
 } rt_scene_info;
 rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 /* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node
@@ -183,17 +185,23 @@ typedef struct {
  * sample and renders it again with a 4096-level stack (rt_stats.resampled).  Only when a level cannot be
  * kept (the megakernel's stack, used for G-buffer/counter renders, or more than 2^20 overflows in one
  * pass) does the render fail: RT_ERR_OVERFLOW, returned by the call that synchronises with it (rt_render
- * with an output pointer, rt_synchronize, rt_get_stats). */
+ * with an output pointer, rt_synchronize, rt_read_accumulation, rt_get_stats).  The outcome accumulates over
+ * asynchronous renders until such a call reads it, so an earlier render's loss is reported even when a
+ * later render lost nothing. */
 rt_status rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* p, uint32_t* out_rgba, float* out_accum);
 /* device pointers of the local accumulation (float4) and RGBA8 buffers */
 rt_status rt_device_buffers(rt_ctx* ctx, void** d_accum, void** d_rgba);
+/* copy the local float4 accumulation (local_rows x W x 4 floats) to host memory after synchronising with
+ * the context's stream; returns RT_ERR_OVERFLOW like rt_synchronize (replaces reading
+ * Renderer::temporal_accumulation_frame_data, MC/Renderer.h:194) */
+rt_status rt_read_accumulation(rt_ctx* ctx, float* out_accum);
 /* copy device RGBA8 to a caller device pointer (e.g. a torch tensor) on the context stream */
 rt_status rt_copy_rgba_to_device(rt_ctx* ctx, void* dst);
 rt_status rt_reset_accumulation(rt_ctx* ctx);
 rt_status rt_synchronize(rt_ctx* ctx);
 
 typedef struct {
-    float last_kernel_ms;     /* megakernel duration of the last rt_render (HIP events, same stream) */
+    float last_kernel_ms;     /* the last rt_render's kernels, first to last (HIP events, same stream) */
     uint64_t node_tests;      /* RT_RENDER_COUNT only */
     uint64_t tri_tests;
     uint64_t rays;
@@ -211,9 +219,12 @@ typedef struct {
     uint32_t n_passes;        /* launches over consecutive frame ranges (bounded parked-sample memory) */
     uint32_t kernel;          /* the path kernel of the last rt_render: RT_KERNEL_* */
     uint64_t resampled;       /* EXACT: samples whose path outgrew the fold ring, rendered again exactly */
-    uint64_t overflow_lost;   /* EXACT: levels / samples that could not be kept (non-zero => RT_ERR_OVERFLOW) */
-    uint32_t pair_cap;        /* vertex kernel (leaf boxes): LDS pair-list entries per wave of the wave-spread
-                                 Moller-Trumbore; 0 = one lane tests its own candidates */
+    uint64_t overflow_lost;   /* EXACT: levels / samples that could not be kept (non-zero => RT_ERR_OVERFLOW)
+                                 -- both summed over the renders since the last synchronisation that checked them */
+    uint32_t pair_cap;        /* reserved (0): the wave-spread Moller-Trumbore pair list was removed */
+    float last_prepass_ms;    /* the vertex kernel's camera pre-pass (camera_prepass_kernel), summed over passes */
+    float last_main_ms;       /* the path kernel proper (pt_coherent_kernel / pt_megakernel), summed over passes;
+                                 last_kernel_ms spans these plus the resample and in-order finalize kernels */
 } rt_stats;
 #define RT_KERNEL_MEGA 0      /* pt_megakernel (rt_kernels.hip): any scene, counters, G-buffer frames */
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */

@@ -1,0 +1,57 @@
+"""bench.py's N > 1 path, run as the driver runs it (torch.distributed.run, one process per rank) with
+two ranks on the box's one GPU: each rank renders its row bands with the HIP kernels, the bands are
+all-gathered (gloo on host-staged bands: RCCL needs one GPU per rank) and reassembled on rank 0; the
+time is the MAX over ranks.  The JSON line must report the whole job (n_gpus 2, both ranks' times, value
+from the slowest) and rank 0's reassembled frame must equal the one-rank frame bit for bit (the RNG is
+keyed by the global pixel).  The RCCL branch itself (one GPU per rank) runs only on a
+multi-GPU node (the driver's scaling run)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from _rt import rt
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W, H, SPP = 96, 70, 8
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_world2_gloo_matches_one_rank(tmp_path):
+    img = tmp_path / "frame.npy"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "2", "--warmup", "1", "--width", str(W), "--height", str(H), "--spp", str(SPP), "--no-cpu-baseline",
+           "--no-fast-probe", "--dump-image", str(img)]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "gloo"
+    ranks = line["rank_elapsed_s"]
+    assert len(ranks) == 2
+    # value is the whole job over the slowest rank's time
+    assert abs(line["value"] - W * H * SPP * 2 / max(ranks) / 1e6) <= 1e-2 * line["value"]
+    assert line["roofline"]["kernel_ms"] > 0
+    gathered = np.load(img)
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        cam, _, _ = rt.camera_default(W, H)
+        one, _ = c.render(cam, SPP, seed=0)
+    finally:
+        c.close()
+    assert np.array_equal(gathered, np.ascontiguousarray(one).view(np.uint32).reshape(H, W))

@@ -87,6 +87,41 @@ def test_device_tree_equals_host_tree(scenes, name):
     print(f"{name}: {tris.shape[0]} triangles, device build {ms:.3f} ms")
 
 
+def negzero_scene():
+    """Triangles whose centroids sit at x = -0.0 (every vertex x is -0.0) in waves of
+    their own, and triangles at negative x: the device's centroid-bound atomics must order -0.0 above every
+    negative float (rt_lbvh.hip atomic_min_f), as the host's fminf does."""
+    rng = np.random.default_rng(7)
+    neg = rng.uniform(-100.0, -50.0, (64, 9)).astype(np.float32)
+    neg[:, 1::3] = rng.uniform(0, 500, (64, 3)); neg[:, 2::3] = rng.uniform(0, 500, (64, 3))
+    nz = rng.uniform(0, 500, (256, 9)).astype(np.float32)
+    nz[:, 0::3] = np.float32(-0.0)
+    sc = rt.Scene()   # (no +0.0 coordinate anywhere: unions of +-0 are not ordered alike by every fminf)
+    sc.add_mesh(np.concatenate([neg, nz]), (0.5, 0.5, 0.5), (0.0, 0.0, 0.0))
+    return sc.build()
+
+
+def test_host_tree_with_negative_zero_centroids_is_well_formed():
+    sc = negzero_scene()
+    nodes, tris = sc.lbvh_host()
+    _, _, tf, ti = sc.export()
+    check_tree(nodes, tris, tf, ti)
+
+
+@pytest.mark.gpu
+def test_device_tree_equals_host_tree_with_negative_zero_centroids():
+    sc = negzero_scene()
+    nodes, tris = sc.lbvh_host()
+    c = rt.Context(0)
+    try:
+        c.upload_gpu_bvh(sc)
+        dn, dt = c.debug_scene_arrays(nodes.shape[0], tris.shape[0])
+    finally:
+        c.close()
+    assert np.array_equal(bits(dn), bits(nodes))
+    assert np.array_equal(bits(dt), bits(tris))
+
+
 @pytest.mark.gpu
 def test_rays_and_image_match_reference_tree(scenes):
     sc = scenes["c5"]

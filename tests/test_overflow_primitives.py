@@ -104,6 +104,28 @@ def test_megakernel_stack_overflow_fails_loudly():
         c.close()
 
 
+def test_overflow_of_an_earlier_async_render_is_reported():
+    """the overflow outcome accumulates over asynchronous renders until a synchronisation reads
+    it -- a clean second render must not mask the first one's loss."""
+    c = context(RT_STACK_DEPTH=2, RT_VERTEX=0, RT_LDS_LEVELS=0)
+    try:
+        c.resize(48, 36)
+        cam, _, _ = rt.camera_default(48, 36)
+        c.render(cam, 24, seed=4, rr=0.9, fetch=False)   # loses levels
+        c.render(cam, 4, seed=5, rr=0.0, fetch=False)    # rr 0: every path ends at its first vertex, no level
+        with pytest.raises(rt.RtError, match="overflow"):
+            c.sync()
+        assert c.stats().overflow_lost > 0
+        # read: the next check is clean again
+        c.render(cam, 4, seed=5, rr=0.0, fetch=False)
+        c.sync()
+        with pytest.raises(rt.RtError, match="overflow"):   # and the read-back entry point reports it too
+            c.render(cam, 24, seed=4, rr=0.9, fetch=False)
+            c.accumulation()
+    finally:
+        c.close()
+
+
 def test_device_primitives_match_reference_fixtures():
     c = rt.Context(0)
     try:

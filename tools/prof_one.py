@@ -43,7 +43,10 @@ def main():
     print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
     if args.sections:
         cyc = c.debug_counters(24)[16:24]
-        names = ["fold drain (top)", "vertex", "finish", "queue + service head", "camera", "box loop", "moller-trumbore", "(entry)"]
+        # rt_coherent.hip SEC_MARK: [0] top (path ends, fold drain, work / camera records), [1] path end (fold set-up,
+        # parked sample), [3] service (shadow verdict, fold level), [4] vertex shading (and the BVH variant's camera
+        # ray), [5] box loop (leaf boxes) or BVH rounds, [6] Moller-Trumbore
+        names = ["top: drain + records", "path end", "(unused)", "service", "vertex", "box loop", "moller-trumbore", "(entry)"]
         tot = float(sum(cyc)) or 1.0
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
         n = c.debug_counters(44)[24:44]
