@@ -611,7 +611,7 @@ class Context:
 
     def math_selftest(self, x):
         x = np.ascontiguousarray(x, np.float32)
-        out = np.zeros((x.shape[0], 7), np.float32)
+        out = np.zeros((x.shape[0], 9), np.float32)
         self._check(lib().rt_math_selftest(self.h, x.shape[0], _fp(x), _fp(out)), "rt_math_selftest")
         return out
 

@@ -1165,12 +1165,12 @@ rt_status rt_math_selftest(rt_ctx* c, uint64_t n, const float* x, float* out)
     HIPC(c, hipSetDevice(c->device));
     float *d_x = nullptr, *d_out = nullptr;
     hipError_t e;
-    if ((e = hipMalloc((void**)&d_x, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 28)) != hipSuccess) {
+    if ((e = hipMalloc((void**)&d_x, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 36)) != hipSuccess) {
         dfree(d_x); dfree(d_out); return hip_fail(c, e, "hipMalloc(selftest)");
     }
     if ((e = hipMemcpyAsync(d_x, x, n * 4, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
         (e = rt_launch_math((uint32_t)n, d_x, d_out, c->stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(out, d_out, n * 28, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, d_out, n * 36, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
         (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
         dfree(d_x); dfree(d_out); return hip_fail(c, e, "rt_math_selftest");
     }

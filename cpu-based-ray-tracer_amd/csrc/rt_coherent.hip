@@ -981,6 +981,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 // compact BVH for an all-finite wave (rt_layout.h): quantized internal boxes (rounded
                 // outward: only extra visits), exact leaf boxes from the triangle's vertices
                 const bool qround = fin && Q.use_qnodes != 0u;
+                // the walk skips a box entered beyond every t that could still matter (exact, DESIGN.md
+                // 5.3): ray A's closest hit so far -- a triangle inside the box hits at t >= its entry, so
+                // it would lose to the current hit (a tie needs entry <= t; the bound keeps 1e-5 relative
+                // margin over the slab's 2e-7 rounding) -- and ray B's light distance (a triangle beyond
+                // it cannot block: MC/Renderer.cpp:184 needs t <= slen - 0.01).  The reference visits every
+                // hit box (MC/BVH.h:82-101); only boxes whose triangles cannot change the result are skipped.
+                const float bound = curA ? ((tA < 1e30) ? (float)tA * 1.00001f + 1e-5f : __builtin_inff()) : slen * 1.00001f + 1e-5f;
                 if (tracing) {
                     uint32_t ti = curA ? tiA : tiB;
                     int parked0 = -1, parked1 = -1;
@@ -995,7 +1002,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                             const float lx = __builtin_fmaf((float)(q.x & 0xFFFFu), sx, ox), hx = __builtin_fmaf((float)(q.x >> 16), sx, ox);
                             const float ly = __builtin_fmaf((float)(q.y & 0xFFFFu), sy, oy), hy = __builtin_fmaf((float)(q.y >> 16), sy, oy);
                             const float lz = __builtin_fmaf((float)(q.z & 0xFFFFu), sz, oz), hz = __builtin_fmaf((float)(q.z >> 16), sz, oz);
-                            const bool hit = slab_hit_finite(r, lx, ly, lz, hx, hy, hz);
+                            const bool hit = slab_hit_finite_within(r, lx, ly, lz, hx, hy, hz, bound);
                             const bool leaf = (q.w & 0x80000000u) != 0u;
                             ti = (hit && !leaf) ? ti + 1 : (leaf ? ti + 1 : q.w);
                             if (hit && leaf) {
@@ -1009,7 +1016,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         for (uint32_t s = 0; s < steps && ti < NN; ++s) {
                             const float4 q0 = S.nodes[2 * ti];
                             const float4 q1 = S.nodes[2 * ti + 1];
-                            const bool hit = decltype(kind)::value ? slab_hit_finite(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y)
+                            const bool hit = decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
                                                                    : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                             const int tri = f2i(q1.w);
                             ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);

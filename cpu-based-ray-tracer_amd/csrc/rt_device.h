@@ -178,6 +178,20 @@ __device__ __forceinline__ bool slab_hit_finite(const Ray& r, float lx, float ly
     const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
     return (tout >= 0.0f) && (tin <= tout);
 }
+// slab_hit_finite, and the box is not entered beyond `bound`: a hit whose entry t exceeds the bound
+// reports a miss.  The entry t is the box's exact entry t up to 3 roundings (relative 2e-7): a caller
+// passes a bound with margin above every t it must keep.
+__device__ __forceinline__ bool slab_hit_finite_within(const Ray& r, float lx, float ly, float lz, float hx, float hy, float hz, float bound)
+{
+    const float ax = r.nx ? hx : lx, bx = r.nx ? lx : hx;
+    const float ay = r.ny ? hy : ly, by = r.ny ? ly : hy;
+    const float az = r.nz ? hz : lz, bz = r.nz ? lz : hz;
+    const float tix = (ax - r.o.x) * r.rcp.x, tiy = (ay - r.o.y) * r.rcp.y, tiz = (az - r.o.z) * r.rcp.z;
+    const float tox = (bx - r.o.x) * r.rcp.x, toy = (by - r.o.y) * r.rcp.y, toz = (bz - r.o.z) * r.rcp.z;
+    const float tin = __builtin_fmaxf(tix, __builtin_fmaxf(tiy, tiz));
+    const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
+    return (tout >= 0.0f) && (tin <= tout) && (tin <= bound);
+}
 __device__ __forceinline__ bool rcp_finite(const Ray& r)
 {
     return __builtin_isfinite(r.rcp.x) && __builtin_isfinite(r.rcp.y) && __builtin_isfinite(r.rcp.z);

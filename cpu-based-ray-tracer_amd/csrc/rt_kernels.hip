@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "rt_device.h"
+#include "rt_glibc_math.h"
 #include "rt_kernels.h"
 #include "rt_path.h"
 
@@ -676,22 +677,25 @@ hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// math self-test kernel: device f32 sqrt/div, f64 reciprocal, cos/sin as the megakernel evaluates them
+// math self-test kernel: device f32 sqrt/div, f64 reciprocal, cos/sin as the megakernel evaluates them,
+// and the denoiser's expf/acosf (rt_glibc_math.h)
 __global__ void math_kernel(uint32_t n, const float* __restrict__ x, float* __restrict__ out)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float v = x[i];
-    out[7 * i + 0] = __builtin_sqrtf(v);
-    out[7 * i + 1] = rcp_f32(v);   // the kernels' reciprocal (rt_device.h); == 1.0f / v correctly rounded
+    out[9 * i + 0] = __builtin_sqrtf(v);
+    out[9 * i + 1] = rcp_f32(v);   // the kernels' reciprocal (rt_device.h); == 1.0f / v correctly rounded
     float cv, sv;
     sincos_f(v, cv, sv);   // what sample_hemisphere evaluates (rt_path.h)
-    out[7 * i + 2] = cv;
-    out[7 * i + 3] = sv;
+    out[9 * i + 2] = cv;
+    out[9 * i + 3] = sv;
     const double r = rcp_f64_of_f32(v);   // Moller-Trumbore's 1 / (double)den (rt_device.h)
-    out[7 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
-    out[7 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));
-    out[7 * i + 6] = pow_lobe(v, 25.0f);   // the C1 specular lobe, powf(x, specular_size_factor = 25)
+    out[9 * i + 4] = __int_as_float((int)(uint32_t)(__double_as_longlong(r) & 0xFFFFFFFFull));
+    out[9 * i + 5] = __int_as_float((int)(uint32_t)((unsigned long long)__double_as_longlong(r) >> 32));
+    out[9 * i + 6] = pow_lobe(v, 25.0f);   // the C1 specular lobe, powf(x, specular_size_factor = 25)
+    out[9 * i + 7] = glibc_math::expf<true>(v);   // the joint bilateral weight's exp (DN/Denoiser.h:203)
+    out[9 * i + 8] = glibc_math::acosf(v);        // its normal-angle acos (DN/Denoiser.h:195)
 }
 
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream)

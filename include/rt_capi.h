@@ -313,7 +313,8 @@ rt_status rt_world_trace(rt_ctx* ctx, uint64_t n, const float* org, const float*
 rt_status rt_debug_primitives(rt_ctx* ctx, uint64_t n_mt, const float* mt_cases, int32_t* mt_hit, double* mt_t, uint64_t n_box,
                               const float* box_cases, int32_t* box_hit);
 /* device arithmetic self-test: for each x: sqrtf, 1/x, cos, sin (as the kernel evaluates them),
- * the double reciprocal's low/high words, and the C1 specular lobe powf(x, 25) -> 7 floats per input */
+ * the double reciprocal's low/high words, the C1 specular lobe powf(x, 25), and the denoiser's expf(x)
+ * and acosf(x) (glibc's algorithms, DN/Denoiser.h:195,203) -> 9 floats per input */
 rt_status rt_math_selftest(rt_ctx* ctx, uint64_t n, const float* x, float* out);
 
 int32_t rt_api_version(void);

@@ -775,6 +775,11 @@ void or_trig(int64_t n, const float* x, float* cos_out, float* sin_out)
     for (int64_t i = 0; i < n; ++i) { cos_out[i] = cosf(x[i]); sin_out[i] = sinf(x[i]); }
 }
 
+void or_exp_acos(int64_t n, const float* x, float* exp_out, float* acos_out)
+{   // the libm the reference's denoiser calls (std::exp / std::acos on float, DN/Denoiser.h:195,203)
+    for (int64_t i = 0; i < n; ++i) { exp_out[i] = expf(x[i]); acos_out[i] = acosf(x[i]); }
+}
+
 uint32_t or_rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim) { return oracle_rng_u32(seed, pixel, frame, dim); }
 float or_rng_float(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim) { return oracle_u32_to_float(oracle_rng_u32(seed, pixel, frame, dim)); }
 

@@ -75,6 +75,7 @@ void or_material_sample(int64_t n, const float* nrm, const float* wi, const uint
 
 /* libm cosf/sinf of n floats */
 void or_trig(int64_t n, const float* x, float* cos_out, float* sin_out);
+void or_exp_acos(int64_t n, const float* x, float* exp_out, float* acos_out);
 
 /* the RNG stream itself (oracle/philox.h) */
 uint32_t or_rng_u32(uint64_t seed, uint32_t pixel, uint32_t frame, uint32_t dim);

@@ -58,6 +58,7 @@ def lib():
         L.or_material_sample.argtypes = [C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_uint32), C.POINTER(C.c_float),
                                          C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.or_trig.argtypes = [C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.or_exp_acos.argtypes = [C.c_int64, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         _lib = L
     return _lib
 
@@ -174,3 +175,11 @@ def libm_trig(x):
     c = np.zeros_like(x); s = np.zeros_like(x)
     lib().or_trig(x.shape[0], _p(x, C.c_float), _p(c, C.c_float), _p(s, C.c_float))
     return c, s
+
+
+def libm_exp_acos(x):
+    """the host libm's expf and acosf (glibc: what the reference's denoiser calls)"""
+    x = np.ascontiguousarray(x, np.float32)
+    e = np.zeros_like(x); a = np.zeros_like(x)
+    lib().or_exp_acos(x.shape[0], _p(x, C.c_float), _p(e, C.c_float), _p(a, C.c_float))
+    return e, a
