@@ -1,0 +1,24 @@
+"""The vertex kernel's compile-time variants still build (CPU; hipcc cross-compiles for gfx950): the section
+timing diagnostics (RT_SECTIONS=1 and the candidate-histogram level 3, tools/prof_one.py) and the
+waves-per-SIMD settings measured in DESIGN.md 6.4.  The product build is the Makefile's; these compile
+rt_coherent.hip alone, device code only, so a diagnostic that is not built by default cannot rot."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.parametrize("flags", ["-DRT_SECTIONS=1", "-DRT_SECTIONS=3", "-DRT_COH_MIN_WAVES=7 -DRT_COH_BVH_MIN_WAVES=7"])
+def test_coherent_kernel_variant_compiles(flags, tmp_path):
+    cmd = [HIPCC, "-std=c++20", "-O3", "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), "-ffp-contract=off",
+           "-fno-fast-math", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+           "-fno-slp-vectorize", "--cuda-device-only", "-c", os.path.join(PKG, "csrc", "rt_coherent.hip"), "-o", str(tmp_path / "k.o")]
+    cmd[1:1] = flags.split()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
