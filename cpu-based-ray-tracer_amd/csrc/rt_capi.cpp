@@ -106,7 +106,7 @@ struct rt_ctx {
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
-    uint32_t vthresh = 40, vsteps = 8; // the same for the vertex kernel's BVH variant (C5 sweep)
+    uint32_t vthresh = 32, vsteps = 8; // the same for the vertex kernel's BVH variant (C5 sweep)
 };
 
 namespace {

@@ -988,6 +988,10 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 // it cannot block: MC/Renderer.cpp:184 needs t <= slen - 0.01).  The reference visits every
                 // hit box (MC/BVH.h:82-101); only boxes whose triangles cannot change the result are skipped.
                 const float bound = curA ? ((tA < 1e30) ? (float)tA * 1.00001f + 1e-5f : __builtin_inff()) : slen * 1.00001f + 1e-5f;
+#if RT_SECTIONS
+                SEC_COUNT(5, 1u);                           // BVH: rounds
+                SEC_COUNT(6, (uint32_t)__popcll(act));     // BVH: lanes tracing per round
+#endif
                 if (tracing) {
                     uint32_t ti = curA ? tiA : tiB;
                     int parked0 = -1, parked1 = -1;
@@ -1029,6 +1033,10 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     if (qround) walk_q();
                     else if (fin) walk(FiniteSlab{});
                     else walk(GeneralSlab{});
+                    SEC_MARK(6);   // BVH: the postponed leaves' tests in the MT section
+#if RT_SECTIONS
+                    SEC_SUM(12, (uint32_t)(parked0 >= 0) + (uint32_t)(parked1 >= 0));   // BVH: leaves tested
+#endif
                     for (int slot = 0; slot < 2; ++slot) {
                         const int pk = slot == 0 ? parked0 : parked1;
                         if (pk < 0 || (!curA && occB)) continue;
@@ -1060,6 +1068,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     }
                     if (curA) tiA = ti;
                     else tiB = ti;
+                    SEC_MARK(5);
                 }
             }
         }

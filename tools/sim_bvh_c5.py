@@ -147,6 +147,32 @@ class Tree:
             kids.sort(key=lambda k: -tin[k])
             stack += kids
         res["wide4"], res["wide4_leaf"] = fetches, leaf_tests
+        # 4-wide in DFS order (no sorting): children of a fetched node pushed in reverse DFS order; the
+        # deepest stack and the box tests (4 per fetch, children that exist)
+        best = np.inf
+        stack = [0]
+        fetches = boxes = leaf_tests = maxst = 0
+        while stack:
+            nidx = stack.pop()
+            if self.tri[nidx] >= 0:
+                leaf_tests += 1
+                if tt[nidx] <= best:
+                    best = tt[nidx]
+                if shadow and tt[nidx] < tmax:
+                    break
+                continue
+            fetches += 1
+            kids = []
+            for ch in (self.left[nidx], self.right[nidx]):
+                if self.tri[ch] >= 0:
+                    kids.append(ch)
+                else:
+                    kids += [self.left[ch], self.right[ch]]
+            boxes += len(kids)
+            kids = [k for k in kids if hit[k] and tin[k] <= bound()]
+            stack += kids[::-1]
+            maxst = max(maxst, len(stack))
+        res["wide4_dfs"], res["wide4_dfs_boxes"], res["wide4_dfs_leaf"], res["wide4_dfs_maxstack"] = fetches, boxes, leaf_tests, maxst
         return res, best_t, (np.argmin(tt) if len(leaves) and np.isfinite(best_t) else -1)
 
 
