@@ -1101,6 +1101,71 @@ template __global__ void pt_coherent_kernel<false, true, false>(KParams);
 // kernel starts the path at its first vertex.  The camera rays of a tile are coherent, so the candidate
 // loop here runs nearly converged, and the vertex kernel spends no iteration on camera rays or on sky
 // samples.
+//
+// The leaf boxes a tile's camera rays can hit: the wave's segment is an 8x8 tile whose rays leave the
+// camera through pixel positions x in [x0, x0 + 8], y in [y0, y1 + 1] (jitter in [0, 1]).  A box that lies
+// wholly outside the frustum through the camera spanned by that pixel rectangle widened by one pixel on
+// every side is hit by none of them: the float ray (RayGen's jitter, NDC, inverse projection, normalize,
+// inverse view) is within ~1e-6 rad of the exact direction and the float slab test within ~1e-7 of the
+// exact entry, while the margin is a pixel (~3e-4 rad at C4), so the box's own slab test -- which alone
+// decides whether the reference tests its triangles (leaf-box monotonicity, rt_scene.cpp) -- fails for
+// every ray of the tile.  Lane b tests box b in double; anything not finite keeps every box.
+__device__ __forceinline__ uint64_t tile_box_mask(const KParams& P, uint32_t lane, double px0, double px1, double py0, double py1)
+{
+    const uint32_t nb = P.n_lboxes;
+    auto dirv = [&](double px, double py, double out[3]) -> bool {
+        const double cx = (px / (double)P.W) * 2.0 - 1.0, cy = (py / (double)P.H) * 2.0 - 1.0;
+        double v[4];
+        for (int i = 0; i < 4; ++i) v[i] = (double)P.iproj[i] * cx + (double)P.iproj[4 + i] * cy + (double)P.iproj[8 + i] + (double)P.iproj[12 + i];
+        if (!(v[3] != 0.0)) return false;
+        const double a = v[0] / v[3], b = v[1] / v[3], c = v[2] / v[3];
+        for (int i = 0; i < 3; ++i) out[i] = (double)P.iview[i] * a + (double)P.iview[4 + i] * b + (double)P.iview[8 + i] * c;
+        return __builtin_isfinite(out[0]) && __builtin_isfinite(out[1]) && __builtin_isfinite(out[2]);
+    };
+    double c[4][3], m[3];
+    bool ok = dirv(px0 - 1.0, py0 - 1.0, c[0]) && dirv(px1 + 1.0, py0 - 1.0, c[1]) && dirv(px1 + 1.0, py1 + 1.0, c[2]) &&
+              dirv(px0 - 1.0, py1 + 1.0, c[3]) && dirv(0.5 * (px0 + px1), 0.5 * (py0 + py1), m);
+    bool keep = true;
+    if (ok && lane < nb) {
+        const float* q = reinterpret_cast<const float*>(P.lboxes) + 8 * (size_t)lane;   // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, masks)
+        const double lo[3] = {(double)q[0] - (double)P.cam_pos[0], (double)q[2] - (double)P.cam_pos[1], (double)q[4] - (double)P.cam_pos[2]};
+        const double hi[3] = {(double)q[1] - (double)P.cam_pos[0], (double)q[3] - (double)P.cam_pos[1], (double)q[5] - (double)P.cam_pos[2]};
+        for (int e = 0; e < 4 && keep; ++e) {
+            const double* u = c[e];
+            const double* w = c[(e + 1) & 3];
+            double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+            if (n[0] * m[0] + n[1] * m[1] + n[2] * m[2] < 0.0) { n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2]; }
+            // the box corner furthest along n: outside when even it is behind the plane
+            const double far = n[0] * (n[0] > 0.0 ? hi[0] : lo[0]) + n[1] * (n[1] > 0.0 ? hi[1] : lo[1]) + n[2] * (n[2] > 0.0 ? hi[2] : lo[2]);
+            if (far < 0.0) keep = false;
+        }
+    }
+    const uint64_t culled = __ballot(ok && lane < nb && !keep);
+    return ~culled;
+}
+
+// one wave per tile: KParams::tile_boxes[tile] for the pre-pass
+__global__ void __launch_bounds__(256) tile_boxes_kernel(KParams P)
+{
+    const uint32_t lane = __lane_id();
+    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (tile >= P.n_tiles) return;   // whole waves
+    const uint32_t trow = tile / P.tiles_x, tcol = tile - trow * P.tiles_x;
+    const uint32_t lr = trow * 8u + (lane >> 3), lx = tcol * 8u + (lane & 7u);
+    const bool valid = lr < P.n_local_rows && lx < P.W;
+    const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
+    const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
+    // the tile's pixel rectangle: x in [x0, x0 + 8], y over its lanes' global rows (row bands)
+    double ylo = valid ? (double)y : 1e30, yhi = valid ? (double)y : -1e30;
+    for (int off = 32; off >= 1; off >>= 1) {
+        ylo = fmin(ylo, __shfl_xor(ylo, off));
+        yhi = fmax(yhi, __shfl_xor(yhi, off));
+    }
+    uint64_t m = ~0ull;
+    if (ylo <= yhi) m = tile_box_mask(P, lane, (double)(tcol * 8u), (double)(tcol * 8u + 8u), ylo, yhi + 1.0);
+    if (lane == 0) P.tile_boxes[tile] = m;
+}
+
 template <bool BVH>
 __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
 {
@@ -1131,6 +1196,8 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
     const uint32_t nf = min(P.seg_frames, P.n_frames - f0);
     const V3 o{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
     float4* const out = P.crec + ((size_t)sg << P.seg_shift);
+    // !BVH: the leaf boxes the tile's frustum meets (tile_boxes_kernel; wave-uniform)
+    const uint64_t boxes = BVH ? ~0ull : P.tile_boxes[tile];
     uint32_t cnt = 0;
     for (uint32_t j = 0; j < nf; ++j) {
         const uint32_t fidx = f0 + j, frame = P.first_frame + fidx;
@@ -1158,7 +1225,9 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
             // the distinct leaf boxes decide the candidates (rt_scene.cpp); Moller-Trumbore in DFS order
             uint64_t cm = 0;
             cbox8* bx = (cbox8*)P.lboxes;
-            for (uint32_t b = 0; b < P.n_lboxes; ++b) {
+            const uint64_t bset = P.n_lboxes >= 64u ? boxes : boxes & ((1ull << P.n_lboxes) - 1ull);
+            for (uint64_t bm = bset; bm != 0; bm &= bm - 1) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(bm);
                 const box8 q = bx[b];
                 const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
                 const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
@@ -1220,8 +1289,12 @@ hipError_t rt_launch_camera_prepass(const KParams& P, bool bvh, size_t lds, hipS
 {
     if (P.n_segments == 0) return hipSuccess;
     const uint32_t blocks = (P.n_segments + 3u) / 4u;
-    if (bvh) hipLaunchKernelGGL(camera_prepass_kernel<true>, dim3(blocks), dim3(256), 0, stream, P);
-    else hipLaunchKernelGGL(camera_prepass_kernel<false>, dim3(blocks), dim3(256), lds, stream, P);
+    if (bvh) {
+        hipLaunchKernelGGL(camera_prepass_kernel<true>, dim3(blocks), dim3(256), 0, stream, P);
+    } else {
+        hipLaunchKernelGGL(tile_boxes_kernel, dim3((P.n_tiles + 3u) / 4u), dim3(256), 0, stream, P);
+        hipLaunchKernelGGL(camera_prepass_kernel<false>, dim3(blocks), dim3(256), lds, stream, P);
+    }
     return hipGetLastError();
 }
 

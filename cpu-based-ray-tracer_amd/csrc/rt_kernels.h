@@ -63,6 +63,7 @@ struct KParams {
     // tag = triangle | pixel-in-tile << 19 | frame-in-chunk << 25 | flipped normal << 31; the non-empty
     // segments are listed in seg_list[0, *seg_list_n) (misses and light hits are parked by the pre-pass)
     float4* crec; uint32_t* ccount; uint32_t* seg_list; uint32_t* seg_list_n;
+    unsigned long long* tile_boxes;   // per tile: the leaf boxes its camera rays' frustum meets (tile_boxes_kernel)
     uint32_t n_segments, n_tiles, seg_frames, seg_shift;
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
