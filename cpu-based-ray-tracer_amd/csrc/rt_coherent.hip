@@ -158,6 +158,16 @@ __device__ __forceinline__ bool box_hit_pk(const f2 sx, const f2 sy, const f2 sz
     const float tout = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax.x, ax.y), __builtin_fmaxf(ay.x, ay.y)), __builtin_fmaxf(az.x, az.y));
     return (tout >= 0.0f) && (tin <= tout);
 }
+// the same, and the box is not entered beyond `bound`: a shadow ray's box entered beyond the light point
+// holds no blocker (a blocker needs t <= slen - 0.01, MC/Renderer.cpp:184, and a triangle inside the box
+// hits at t >= its entry; the bound keeps 1e-5 relative margin over the entry's 2e-7 rounding)
+__device__ __forceinline__ bool box_hit_pk_within(const f2 sx, const f2 sy, const f2 sz, const V3& rc, float bound)
+{
+    const f2 ax = sx * f2{rc.x, rc.x}, ay = sy * f2{rc.y, rc.y}, az = sz * f2{rc.z, rc.z};
+    const float tin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(ax.x, ax.y), __builtin_fminf(ay.x, ay.y)), __builtin_fminf(az.x, az.y));
+    const float tout = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(ax.x, ax.y), __builtin_fmaxf(ay.x, ay.y)), __builtin_fmaxf(az.x, az.y));
+    return (tout >= 0.0f) && (tin <= tout) && (tin <= bound);
+}
 
 // a finished sample's radiance into its parked slot (4-frame blocks: the 4 frames of a block of one pixel
 // are 48 contiguous bytes); finalize_chunks_kernel accumulates every pixel's samples in frame order
@@ -810,12 +820,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             // a box is one 32-byte scalar load (s_load_dwordx8; a group of BOX_UNROLL boxes waits once)
             cbox8* bx = (cbox8*)kargs4().lboxes;
             const uint32_t nb = kargs4().n_lboxes;
+            const float bndB = slen * 1.00001f + 1e-5f;   // ray B: no blocker in a box entered beyond the light point
             auto one_box = [&](const box8 q) {   // (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, mask 0-31, mask 32-63), rt_layout.h
                 // (lo - o, hi - o) per axis in the halves of packed registers, shared by the two rays
                 const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
                 const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
                 const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
-                const bool hA = box_hit_pk(sx, sy, sz, rA), hB = box_hit_pk(sx, sy, sz, rB);
+                const bool hA = box_hit_pk(sx, sy, sz, rA), hB = box_hit_pk_within(sx, sy, sz, rB, bndB);
                 const uint32_t m0 = (uint32_t)f2i(q.s6);
                 if (NARROW) {
                     ma |= hA ? m0 : 0u;
