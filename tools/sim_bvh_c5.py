@@ -173,6 +173,34 @@ class Tree:
             stack += kids[::-1]
             maxst = max(maxst, len(stack))
         res["wide4_dfs"], res["wide4_dfs_boxes"], res["wide4_dfs_leaf"], res["wide4_dfs_maxstack"] = fetches, boxes, leaf_tests, maxst
+        # the kernel's wide walk (rt_coherent.hip walk_w): leaves postponed, the first hit internal slot next,
+        # the others pushed in slot order onto a 4-entry stack; a push past it = overflow (binary restart)
+        best = np.inf
+        cur, st, fetches, over = 0, [], 0, 0
+        while cur is not None:
+            fetches += 1
+            kids = []
+            for ch in (self.left[cur], self.right[cur]):
+                kids += [ch] if self.tri[ch] >= 0 else [self.left[ch], self.right[ch]]
+            nxt = None
+            for k in kids:
+                if not (hit[k] and tin[k] <= bound()):
+                    continue
+                if self.tri[k] >= 0:
+                    if tt[k] <= best:
+                        best = tt[k]
+                elif nxt is None:
+                    nxt = k
+                elif len(st) < 4:
+                    st.append(k)
+                else:
+                    over = 1
+            if over:
+                break
+            if nxt is None and st:
+                nxt = st.pop()
+            cur = nxt
+        res["walk_w_fetches"], res["walk_w_overflow"] = fetches, over
         return res, best_t, (np.argmin(tt) if len(leaves) and np.isfinite(best_t) else -1)
 
 
