@@ -262,10 +262,9 @@ def main():
     per_rank = [elapsed]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
-        if gloo:
-            parts = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
-            dist.all_gather(parts, t)
-            per_rank = [float(x.item()) for x in parts]
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        per_rank = [float(x.item()) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_samples = W * H * spp * args.steps

@@ -826,11 +826,16 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 HIPC(c, hipEventRecord(c->kev[3 * pass], c->stream));
                 if (coh_box) {
                     // the leaf-box variant's camera pre-pass: segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
+                    Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
                     uint32_t lf = 0;
                     while ((1u << lf) < nf && lf < 6) ++lf;
+                    // a wave of the path kernel takes whole segments: keep at least 32 per wave, so the
+                    // launch's tail (the waves' last segments) stays short when a pass has few tiles (a
+                    // rank's row bands of a multi-GPU frame: 8 ranks at C4 -> 16-frame segments)
+                    const uint64_t waves = (uint64_t)grid * (c->block / 64u);
+                    while (lf > 3 && (uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) < 32u * waves) --lf;
                     Q.seg_frames = 1u << lf;
                     Q.seg_shift = 6 + lf;
-                    Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
                     const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);
                     if (nseg >= (1ull << (32 - Q.seg_shift))) { c->err = "too many samples for one pass"; return RT_ERR_INVALID; }
                     Q.n_segments = (uint32_t)nseg;

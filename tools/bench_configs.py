@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Per-configuration throughput on ONE MI355X.
 
-bench.py reports the headline (C4); this prints one JSON line per configuration with the megakernel
-time (HIP events on its stream), Msamples/s, and the algorithmic-bytes roofline of SURVEY.md 8(d)
-(reference work per sample x measured samples/s vs 8 TB/s).  C5 runs at a reduced spp (frames are
-i.i.d. and the kernel time is linear in spp); the spp used is in each line.
+bench.py reports the headline (C4); this prints one JSON line per configuration with the render's kernel
+time (HIP events on its stream), Msamples/s, and for the path-traced configs the VALU roofline bench.py
+uses: the REFERENCE's work per sample (rays, node and triangle tests per ray, shading
+calls) priced at 18 flops per box test, 54 per triangle test and 150 per shading call, against the
+157.3 TFLOP/s fp32 VALU peak.  (The scene is on chip for C2/C4; C5's traffic is in its PMC summary,
+DESIGN.md 5.1.)  C5 runs at a reduced spp (frames are i.i.d. and the kernel time is linear in spp); the spp
+used is in each line.
 
     python tools/bench_configs.py                 # all configs
     python tools/bench_configs.py --configs C5 --c5-spp 64
@@ -20,16 +23,17 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from _rt import rt  # noqa: E402
 
-HBM_PEAK = 8000.0
-# reference work per sample, SURVEY.md 8(d): rays/sample, node tests/ray, triangle tests/ray
-WORK = {"C1": None, "C2": (5.700, 27.84, 4.06), "C3": (1.446, 38.26, 2.57), "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
+VALU_PEAK_TFLOPS = 157.3
+# reference work per sample, SURVEY.md 8(d): rays/sample, node tests/ray, triangle tests/ray; shading calls
+# per sample measured for C4 (1.4723 = 0.4036 per ray) and scaled by rays for C2/C5
+WORK = {"C1": None, "C2": (5.700, 27.84, 4.06), "C3": None, "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
 
 
-def bytes_per_sample(c):
-    if WORK[c] is None:   # C1: three entities, no BVH; brute force over 2 spheres + 2 triangles
+def flops_per_sample(c):
+    if WORK[c] is None:   # C1 / C3: Whitted renders (one primary ray per pixel, no path sampling)
         return None
     r, n, t = WORK[c]
-    return r * (n * 32 + t * 36 + 16)
+    return r * (n * 18 + t * 54) + 0.4036 * r * 150
 
 
 def run(ctx, cam, W, H, spp, reps, **kw):
@@ -101,9 +105,9 @@ def main():
         st = ctx.stats()
         samples = W * H * spp
         rate = samples / (ms / 1e3)
-        bps = bytes_per_sample(c)
-        roof = None if bps is None else {"bytes_per_sample": round(bps, 1), "achieved_gbs": round(bps * rate / 1e9, 1),
-                                         "peak_gbs": HBM_PEAK, "frac": round(bps * rate / 1e9 / HBM_PEAK, 4)}
+        fps = flops_per_sample(c)
+        roof = None if fps is None else {"bound": "valu", "flops_per_sample": round(fps, 1), "achieved_tflops": round(fps * rate / 1e12, 3),
+                                         "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(fps * rate / 1e12 / VALU_PEAK_TFLOPS, 4)}
         print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
                           "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "roofline": roof,
                           "mode": "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")}), flush=True)
