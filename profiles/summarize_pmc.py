@@ -83,7 +83,8 @@ def main():
     ap.add_argument("dst")
     ap.add_argument("--key", required=True, help="bench.py traffic key (WxHxSPP_mode_nN_pP; stored as KERNEL:key)")
     ap.add_argument("--samples", type=float, required=True, help="samples per megakernel launch")
-    ap.add_argument("--kernel", default="pt_megakernel")
+    ap.add_argument("--kernel", default="pt_megakernel", help="substring of the profiled kernel's name (e.g. 'pt_coherent_kernel<true')")
+    ap.add_argument("--key-kernel", default=None, help="kernel name in the stored key (bench.py's KERNEL_NAMES); default --kernel")
     ap.add_argument("--sha", default=None, help="lib_sha256 of the profiled build (bench line); default: the in-tree librt_hip.so")
     args = ap.parse_args()
     os.makedirs(args.dst, exist_ok=True)
@@ -100,7 +101,7 @@ def main():
     for f in glob.glob(os.path.join(args.src, "trace", "**", "*kernel_stats.csv"), recursive=True):
         stats = list(csv.DictReader(open(f)))
     lib = os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so")
-    out = {"kernel": args.kernel, "key": args.kernel + ":" + args.key, "per_launch_counters": counters, "samples_per_launch": args.samples,
+    out = {"kernel": args.kernel, "key": (args.key_kernel or args.kernel) + ":" + args.key, "per_launch_counters": counters, "samples_per_launch": args.samples,
            "lib_sha256": args.sha or (hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None)}
     if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
         hbm = counters["FETCH_SIZE"] * 1024 * 2 + counters["WRITE_SIZE"] * 1024
