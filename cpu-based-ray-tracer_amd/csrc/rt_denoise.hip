@@ -99,7 +99,7 @@ __device__ __forceinline__ JbfConsts jbf_consts(const DenoiseParams& D)
     K.dsk = 2.0f * D.sigma_coplanarity * D.sigma_coplanarity;
     K.ysp = rcp_f32(K.dsp); K.ysc = rcp_f32(K.dsc); K.ysn = rcp_f32(K.dsn); K.ysk = rcp_f32(K.dsk);
     auto ok = [](float d) { return d >= 0x1p-20f && d < 0x1p20f; };   // div_fast's verified divisor range
-    K.fast = ok(K.dsp) && ok(K.dsc) && ok(K.dsn) && ok(K.dsk);
+    K.fast = ok(K.dsp) && ok(K.dsc) && ok(K.dsn) && ok(K.dsk) && D.ieee_div == 0;
     return K;
 }
 
@@ -299,12 +299,14 @@ hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream)
     const uint32_t tiles = (uint32_t)(((D.W + 15) / 16) * ((D.H + 15) / 16));
     if (tiles == 0) return hipSuccess;
     if (D.jbf_half > 0) {
+        DenoiseParams Dl = D;
+        Dl.ieee_div = getenv("RT_JBF_IEEE") ? 1 : 0;   // diagnostic: every division by the IEEE sequence (tests)
         if (D.jbf_half <= JB_MAX_HALF && !getenv("RT_JBF_GLOBAL")) {
             const uint32_t blocks = (uint32_t)(((D.W + JBW - 1) / JBW) * ((D.H + JBH - 1) / JBH));
             const size_t lds = (size_t)9 * JSLOTS * jbf_pitch(D.jbf_half) * sizeof(float);
-            hipLaunchKernelGGL(jbf_lds_kernel, dim3(blocks), dim3(256), lds, stream, D);
+            hipLaunchKernelGGL(jbf_lds_kernel, dim3(blocks), dim3(256), lds, stream, Dl);
         } else {
-            hipLaunchKernelGGL(jbf_kernel, dim3(tiles), dim3(256), 0, stream, D);
+            hipLaunchKernelGGL(jbf_kernel, dim3(tiles), dim3(256), 0, stream, Dl);
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;

@@ -121,6 +121,7 @@ struct DenoiseParams {
     int jbf_half; float sigma_position, sigma_color, sigma_normal, sigma_coplanarity; int immediate_clamp;
     int temporal_half; float tolerance, weighting; int have_prev;
     float prev_proj[16], prev_view[16];
+    int ieee_div;   // diagnostic (RT_JBF_IEEE): the filter's divisions by the IEEE sequence, not Markstein's correction
 };
 hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream);
 

@@ -112,3 +112,33 @@ def test_restart_drops_the_history(fixture):
         assert np.array_equal(bits(out[..., :3]), bits(z[f"{name}_f2_color"]))   # == this frame's G-buffer color
     finally:
         ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sig", [(32.0, 0.6, 0.1, 0.1), (1.7, 0.23, 0.41, 0.05), (0.3, 2.5, 0.02, 0.9), (1e-4, 0.6, 0.1, 0.1)])
+def test_markstein_divisions_equal_ieee(sig, monkeypatch):
+    """The filter divides by 2 sigma^2 with Markstein's correction from the correctly rounded reciprocal
+    (rt_denoise.hip jbf_div) when every divisor is in [2^-20, 2^20), the IEEE sequence otherwise.  The
+    reference's sigmas are private constants (DN/Denoiser.h:353-356), so only the defaults have golden
+    frames (test_denoised_frames); for other sigmas this checks the shortcut against the IEEE divisions
+    on the same G-buffer (RT_JBF_IEEE), bit for bit -- the last set's 2e-8 divisor takes the IEEE path."""
+    W, H = 96, 72
+    sp, sc, sn, sk = sig
+    out = []
+    for ieee in (False, True):
+        if ieee:
+            monkeypatch.setenv("RT_JBF_IEEE", "1")
+        else:
+            monkeypatch.delenv("RT_JBF_IEEE", raising=False)
+        c = rt.Context(0)
+        try:
+            c.upload(rt.Scene.cornell())
+            c.resize(W, H)
+            params = rt.denoise_params(jbf_half_size=7, temporal_half_size=0, sigma_position=sp, sigma_color=sc, sigma_normal=sn,
+                                       sigma_coplanarity=sk)
+            cam, proj, view = rt.camera_look_ex(W, H, rt.DEFAULT_CAMERA_POSITION, FWD)
+            c.render_denoised(cam, proj, view, 1, params, seed=4)
+            out.append(c.gbuffer()["spatial"][..., :3].copy())
+        finally:
+            c.close()
+    assert np.array_equal(bits(out[0]), bits(out[1]))
