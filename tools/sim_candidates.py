@@ -144,7 +144,7 @@ def main():
     o = np.zeros((NL, 3)); dA = np.zeros((NL, 3)); dB = np.zeros((NL, 3))
     hasA = np.zeros(NL, bool); hasB = np.zeros(NL, bool)
     slen = np.zeros(NL); sc2 = np.zeros(NL)
-    stats = {k: [] for k in ["lanesA", "lanesB", "nA", "nB", "L0", "L_Aonly", "L_Bonly", "sel_min_tin", "L_mayhit", "L_2phase", "L_2phase_B", "L_tcullA_box", "mayA", "mayB", "survA", "survB"]}
+    stats = {k: [] for k in ["lanesA", "lanesB", "nA", "nB", "L0", "L_Aonly", "L_Bonly", "sel_min_tin", "L_mayhit", "L_2phase", "L_2phase_B", "L_tcullA_box", "L_near2", "mayA", "mayB", "survA", "survB"]}
     for it in range(a.iters):
         # new camera rays for lanes without a path
         new = ~in_path
@@ -264,6 +264,17 @@ def main():
         stats["L_2phase"].append(wmax(nsA + nsB).mean())
         stats["L_2phase_B"].append(wmax(nA + nsB).mean())
         stats["L_tcullA_box"].append(wmax(nA_box + nB).mean())
+        # A: the nearest hit box's triangles first; the rest only when that hit is not before the second
+        # nearest hit box's entry (the kernel's two-level form: no per-box entry kept past the box loop)
+        tin_h = np.where(hitA, tinA, np.inf)
+        ordb = np.argsort(tin_h, axis=1)
+        b1 = ordb[:, 0]; t2 = tin_h[np.arange(NL), ordb[:, 1]]
+        in1 = box_of_tri[None, :] == b1[:, None]
+        m1 = candA & in1
+        best1 = np.min(np.where(m1 & hitTA, tA, np.inf), axis=1)
+        restA = candA & ~in1
+        nA_near2 = m1.sum(1) + np.where(best1 < t2 * (1 - 1e-4) - 1e-4, 0, restA.sum(1))
+        stats["L_near2"].append(wmax(nA_near2 + nB).mean())
         stats["mayA"].append(mayA.sum() / max(1, hasA.sum())); stats["mayB"].append(mayB.sum() / max(1, hasB.sum()))
         stats["survA"].append(nsA.sum() / max(1, hasA.sum())); stats["survB"].append(nsB.sum() / max(1, hasB.sum()))
         stats["sel_min_tin"].append(0)
