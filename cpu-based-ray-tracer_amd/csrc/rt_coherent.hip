@@ -1124,11 +1124,17 @@ template __global__ void pt_coherent_kernel<false, true, false>(KParams);
 __device__ __forceinline__ uint64_t tile_box_mask(const KParams& P, uint32_t lane, double px0, double px1, double py0, double py1)
 {
     const uint32_t nb = P.n_lboxes;
+    // the rectangle's directions form a convex cone when the homogeneous w keeps one sign over it (a
+    // perspective inverse: w does not depend on the pixel at all); otherwise nothing is culled
+    int wsign = 0;
     auto dirv = [&](double px, double py, double out[3]) -> bool {
         const double cx = (px / (double)P.W) * 2.0 - 1.0, cy = (py / (double)P.H) * 2.0 - 1.0;
         double v[4];
         for (int i = 0; i < 4; ++i) v[i] = (double)P.iproj[i] * cx + (double)P.iproj[4 + i] * cy + (double)P.iproj[8 + i] + (double)P.iproj[12 + i];
         if (!(v[3] != 0.0)) return false;
+        const int sg = v[3] > 0.0 ? 1 : -1;
+        if (wsign != 0 && sg != wsign) return false;
+        wsign = sg;
         const double a = v[0] / v[3], b = v[1] / v[3], c = v[2] / v[3];
         for (int i = 0; i < 3; ++i) out[i] = (double)P.iview[i] * a + (double)P.iview[4 + i] * b + (double)P.iview[8 + i] * c;
         return __builtin_isfinite(out[0]) && __builtin_isfinite(out[1]) && __builtin_isfinite(out[2]);

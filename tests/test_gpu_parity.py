@@ -351,3 +351,34 @@ def test_vertex_bvh_kernel_equals_megakernel(monkeypatch, scene, exact):
     for name in ("mega", "vertex_chunks"):
         assert np.array_equal(out[name][0], out["vertex"][0]), name
         assert np.array_equal(bits(out[name][1]), bits(out["vertex"][1])), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("view", [((2.78, 2.73, -8.0), (0.0, 0.0, 1.0), 35.0),      # the usual view, centred
+                                  ((2.78, 1.0, 2.8), (0.0, 1.0, 0.0), 90.0),       # inside the box, up at the light
+                                  ((0.3, 0.3, 0.3), (0.6, 0.35, 0.7), 110.0),      # a corner, very wide
+                                  ((4.2, 0.8, 4.0), (-0.3, 0.05, -0.9), 20.0),     # inside the tall block's box, narrow
+                                  ((2.78, 9.0, 2.8), (0.0, -1.0, 0.001), 60.0)])   # above the ceiling, looking down
+def test_prepass_tile_cull_views(view):
+    """The camera pre-pass tests only the leaf boxes its tile's frustum meets (rt_coherent.hip
+    tile_box_mask): over cameras inside and outside the box, wide and narrow, looking along an axis, the
+    vertex kernel's image equals the megakernel's (which tests every box for every ray) bit for bit."""
+    pos, fwd, fov = view
+    W, H, spp = 200, 120, 6
+    cam = rt.camera_look(W, H, pos, fwd, vfov=fov)
+    out = []
+    for vertex in ("1", "0"):
+        os.environ["RT_VERTEX"] = vertex
+        try:
+            c = rt.Context(0)
+            try:
+                c.upload(rt.Scene.cornell())
+                c.resize(W, H)
+                _, acc = c.render(cam, spp, seed=7)
+                out.append((acc, c.stats().kernel))
+            finally:
+                c.close()
+        finally:
+            os.environ.pop("RT_VERTEX", None)
+    assert out[0][1] == 1 and out[1][1] == 0
+    assert np.array_equal(bits(out[0][0]), bits(out[1][0]))
