@@ -119,14 +119,15 @@ __device__ __forceinline__ void jbf_store(const DenoiseParams& D, int i, V3 acc,
 // holds 9 planes (color, position, normal; a pixel outside the image or not a contributor carries a NaN
 // normal x and is skipped, as the reference's window bounds and contributor test skip it).  Plane pitch
 // CHP = 4 (mod 32) keeps a ds_read_b32 lane group (4 rows x 8 slots) on distinct banks.
-constexpr int JBW = 8, JBH = 32, JSLOTS = JBW + 1, JB_MAX_HALF = 80;
+constexpr int JBW = 8, JSLOTS = JBW + 1, JB_MAX_HALF = 80;
 
-__host__ __device__ inline int jbf_pitch(int h) { const int ch = JBH + 2 * h; return ch + ((4 - ch % 32) + 32) % 32; }
+__host__ __device__ inline int jbf_pitch(int jbh, int h) { const int ch = jbh + 2 * h; return ch + ((4 - ch % 32) + 32) % 32; }
 
-__global__ void __launch_bounds__(256) jbf_lds_kernel(DenoiseParams D)
+template <int JBH>
+__global__ void __launch_bounds__(8 * JBH) jbf_lds_kernel(DenoiseParams D)
 {
     extern __shared__ float lds[];
-    const int h = D.jbf_half, CH = JBH + 2 * h, CHP = jbf_pitch(h);
+    const int h = D.jbf_half, CH = JBH + 2 * h, CHP = jbf_pitch(JBH, h);
     const int tiles_x = (D.W + JBW - 1) / JBW;
     const int x0 = (int)(blockIdx.x % (uint32_t)tiles_x) * JBW, y0 = (int)(blockIdx.x / (uint32_t)tiles_x) * JBH;
     const int lane = (int)(threadIdx.x & 63u), wv = (int)(threadIdx.x >> 6);
@@ -302,9 +303,16 @@ hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream)
         DenoiseParams Dl = D;
         Dl.ieee_div = getenv("RT_JBF_IEEE") ? 1 : 0;   // diagnostic: every division by the IEEE sequence (tests)
         if (D.jbf_half <= JB_MAX_HALF && !getenv("RT_JBF_GLOBAL")) {
-            const uint32_t blocks = (uint32_t)(((D.W + JBW - 1) / JBW) * ((D.H + JBH - 1) / JBH));
-            const size_t lds = (size_t)9 * JSLOTS * jbf_pitch(D.jbf_half) * sizeof(float);
-            hipLaunchKernelGGL(jbf_lds_kernel, dim3(blocks), dim3(256), lds, stream, Dl);
+            // 8 x 64 blocks (8 waves) for wide windows: the ring's halo rows are shared by twice the pixels
+            // and 6 waves per SIMD fit instead of 4 (DN65 13.8 -> 12.6 ms); 8 x 32 below a half width of 24
+            // (DN33 3.41 ms against 3.66); the 8 x 64 ring must fit 64 KiB of LDS: half widths up to 64.
+            // RT_JBF_TALL=32/64 forces one (A/B, tests)
+            const int want = getenv("RT_JBF_TALL") ? atoi(getenv("RT_JBF_TALL")) : (D.jbf_half >= 24 ? 64 : 32);
+            const int jbh = (want == 64 && D.jbf_half <= 64) ? 64 : 32;
+            const uint32_t blocks = (uint32_t)(((D.W + JBW - 1) / JBW) * ((D.H + jbh - 1) / jbh));
+            const size_t lds = (size_t)9 * JSLOTS * jbf_pitch(jbh, D.jbf_half) * sizeof(float);
+            if (jbh == 64) hipLaunchKernelGGL(jbf_lds_kernel<64>, dim3(blocks), dim3(512), lds, stream, Dl);
+            else hipLaunchKernelGGL(jbf_lds_kernel<32>, dim3(blocks), dim3(256), lds, stream, Dl);
         } else {
             hipLaunchKernelGGL(jbf_kernel, dim3(tiles), dim3(256), 0, stream, Dl);
         }

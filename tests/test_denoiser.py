@@ -55,15 +55,17 @@ def test_params_defaults_are_the_reference_members():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["lds", "global"])
+@pytest.mark.parametrize("path", ["lds32", "lds64", "global"])
 @pytest.mark.parametrize("case", ["full", "temporal", "jbf16"])
 def test_denoised_frames(fixture, case, path, monkeypatch):
-    """path: the LDS-ring filter (jbf_lds_kernel, the default) or the direct-gather one (jbf_kernel, taken
-    for windows wider than the ring; RT_JBF_GLOBAL forces it)"""
+    """path: the LDS-ring filter (jbf_lds_kernel, the default) with 8 x 32 or 8 x 64 pixel blocks
+    (RT_JBF_TALL), or the direct-gather one (jbf_kernel, taken for windows wider than the ring;
+    RT_JBF_GLOBAL forces it)"""
     if path == "global":
         monkeypatch.setenv("RT_JBF_GLOBAL", "1")
     else:
         monkeypatch.delenv("RT_JBF_GLOBAL", raising=False)
+        monkeypatch.setenv("RT_JBF_TALL", path[3:])
     z = fixture
     name, W, H, n, seed, jh, th, clamp, tol, wgt = next(c for c in cases(z) if c[0] == case)
     ctx = rt.Context(0)
