@@ -213,13 +213,23 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #define RT_SEC_COUNTS 20
 
 // Tuned constants (A/B history: DESIGN.md 6.4, profiles/r02/ab/):
-//  * leaf boxes per scalar-load group in the box loop (one wait per 4 boxes; +0.9 % C4 over 1);
+//  * leaf boxes per scalar-load group in the box loop (round 2: 4 boxes per wait +0.9 % over 1; after the
+//    pre-pass and the tile cull, 1 box per wait +2.3 % over 4 at C4, profiles/r03/ab/ab_c4_box_unroll.json);
 //  * fold levels drained per iteration at the top of the loop, their ring loads issued together (a fold
 //    then rarely still drains when the next path ends): C4 1 level 5935, 2 6117, 3 6198, 4 6195 Msamples/s;
 //  * ring levels loaded together when a fold is completed at once (drain_all).
-constexpr int BOX_UNROLL = 4;
-constexpr uint32_t DRAIN_STEP = 3;
-constexpr uint32_t DRAIN_BATCH = 2;
+#ifndef RT_BOX_UNROLL
+#define RT_BOX_UNROLL 1
+#endif
+#ifndef RT_DRAIN_STEP
+#define RT_DRAIN_STEP 3
+#endif
+#ifndef RT_DRAIN_BATCH
+#define RT_DRAIN_BATCH 2
+#endif
+constexpr int BOX_UNROLL = RT_BOX_UNROLL;
+constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
+constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
 // fold ring layout: lane-major ([thread][position]): a lane's consecutive levels share cache lines, so a
 // drain read follows its push in L2
 #define RING_AT(p) ((size_t)gtid * Q.stack_depth + (p))
