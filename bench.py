@@ -151,9 +151,10 @@ def cpu_baseline(W, H, seconds):
                 for i in range(raw.shape[0]):
                     f.write("f %d %d %d\n" % (3 * i + 1, 3 * i + 2, 3 * i + 3))
 
-        def run(spp):
-            r = subprocess.run([harness, "bench_mt", tmp, "", str(W), str(H), str(spp), "0.8", str(threads)],
-                               check=True, capture_output=True, text=True)
+        def run(spp, nthreads=threads, cpus=None):
+            r = subprocess.run([harness, "bench_mt", tmp, "", str(W), str(H), str(spp), "0.8", str(nthreads)],
+                               check=True, capture_output=True, text=True,
+                               preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
             tok = r.stdout.split()
             return int(tok[2]), float(tok[4])   # samples, seconds (the frames only; scene build excluded)
 
@@ -163,6 +164,18 @@ def cpu_baseline(W, H, seconds):
         rate = n / dt / 1e6
         per_thread = rate / threads
         est = per_thread * cpu["physical_cores_per_socket"]
+        # what SMT adds to a core (the estimate above runs one thread per physical core): one thread on a
+        # core against two on its SMT siblings, ~2 s each, when the affinity mask holds a sibling pair
+        smt = None
+        sib = [int(c) for c in (cpu["cpu0_smt_siblings"] or "").replace("-", ",").split(",") if c.strip().isdigit()]
+        aff = os.sched_getaffinity(0)
+        if len(sib) >= 2 and sib[0] in aff and sib[1] in aff:
+            spp1 = max(1, int(2.0 * per_thread * 1e6 / (W * H)))
+            na, ta = run(spp1, 1, [sib[0]])
+            nb, tb = run(2 * spp1, 2, sib[:2])
+            gain = (nb / tb) / (na / ta)
+            smt = {"cpus": sib[:2], "gain": round(gain, 3), "value": round(est * gain, 2),
+                   "how": "the one-thread-per-core estimate x the throughput two SMT siblings add over one thread on their core"}
         return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
                 "rng": "shipped (thread_local mt19937 seed 5489, MSVC 32-bit distribution, persistent pool)",
                 "cpu_model": cpu["model"], "sockets": cpu["sockets"],
@@ -171,6 +184,7 @@ def cpu_baseline(W, H, seconds):
                 "socket_estimate": {"value": round(est, 2), "threads": cpu["physical_cores_per_socket"],
                                     "how": f"measured {per_thread:.4f} Msamples/s per thread at {threads} threads x "
                                            f"{cpu['physical_cores_per_socket']} physical cores of one socket (linear)"},
+                "socket_estimate_smt": smt,
                 "sample": f"oracle/_ref/ref_harness bench_mt: the reference's MC/ BVH, triangle, material and camera code "
                           f"(compiled from /root/reference), integrator glue restated, shipped RNG; Cornell {W}x{H} x "
                           f"{spp} spp = {n} samples in {dt:.1f} s on {threads} threads (this job's CPU share), RR 0.8"}
@@ -330,6 +344,8 @@ def main():
         if cpu is not None:
             cpu["gpu_over_cpu"] = round(value / cpu["value"], 1)
             cpu["gpu_over_socket_estimate"] = round(value / cpu["socket_estimate"]["value"], 1)
+            if cpu.get("socket_estimate_smt"):
+                cpu["gpu_over_socket_estimate_smt"] = round(value / cpu["socket_estimate_smt"]["value"], 1)
 
     if rank == 0:
         line = {
