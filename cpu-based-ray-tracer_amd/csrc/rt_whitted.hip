@@ -13,7 +13,8 @@
 //     total_specular * phong_specular with phong_specular == 0 for every mesh of the scene
 //     (BV/TriangleMesh.h:139); it adds +0 to a non-negative color and is not evaluated;
 //   * accumulation, average, clamp and ABGR8 pack as RayGen_Shader.
-// The scene (1.4 MB for C3) is read from HBM through L2; one thread per local pixel in 16x16 tiles.
+// The scene (1.4 MB for C3) is read from HBM through L2; a block per 8x8 tile of local pixels, one wave per
+// group of frames (whitted_kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,116 +26,186 @@ using namespace rtd;
 
 namespace {
 
+// box tests per round of the C3 walk; a round's hit leaves (two at most) are postponed to its end, so a
+// wave runs Moller-Trumbore once per round (8: 6044 Msamples/s; 4: 5681, 16: 5729;
+// profiles/r03/ab/ab_c3_whitted.json)
+#ifndef RT_WH_STEPS
+#define RT_WH_STEPS 8
+#endif
+struct FiniteSlab { static constexpr bool value = true; };
+struct GeneralSlab { static constexpr bool value = false; };
+
 // closest hit (shadow == false) or "any hit with t*t < d2" (shadow == true) over the global scene
 template <bool COUNT>
 __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r, bool shadow, double d2, double& best, int& best_tri, bool& occluded,
                                                  uint32_t& node_tests, uint32_t& tri_tests)
 {
+    // A box entered beyond every t that can still change the result is skipped (the C5 walk's rule,
+    // rt_coherent.hip): a triangle inside the box hits at t >= the box's exact entry, and the float entry
+    // is that value up to 3 roundings (2e-7 relative), so with 1e-5 relative margin only boxes whose
+    // triangles lose are skipped -- to the closest hit so far (a tie needs t == best: entry <= best), or,
+    // for a shadow ray, to the light (occluded needs t * t < d2, BV/Renderer.cpp:195, so t < sqrt(d2)).
+    // The reference visits every hit box (BV/BVH.h:82-101).  Rays with a non-finite reciprocal keep the
+    // std::max/min slab test and visit every hit box.
     const float4* __restrict__ nodes = P.nodes;
     const float4* __restrict__ tris = P.tris;
     const uint32_t n = P.n_nodes;
-    uint32_t i = 0;
-    while (i < n) {
-        const float4 q0 = nodes[2 * i];
-        const float4 q1 = nodes[2 * i + 1];
-        if (COUNT) ++node_tests;
-        const bool hit = slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
-        const int tri = f2i(q1.w);
-        const uint32_t skip = (uint32_t)f2i(q1.z);
-        if (hit && tri >= 0) {
-            if (COUNT) ++tri_tests;
-            const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
-            double t;
-            if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
-                if (shadow) {
-                    // (shadow_record.has_intersection) && (t * t < light_distance_squared), BV/Renderer.cpp:195
-                    if (t * t < d2) { occluded = true; return; }
-                } else if (t <= best) {
-                    best = t; best_tri = tri;   // (left.t < right.t) ? left : right: the later leaf wins ties
-                }
+    const float sbound = shadow ? __builtin_sqrtf((float)d2) * 1.00001f + 1e-5f : 0.0f;
+    auto tri_test = [&](int tri) -> bool {   // true: the shadow ray is occluded (the walk ends)
+        if (COUNT) ++tri_tests;
+        const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
+        double t;
+        if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
+            if (shadow) {
+                // (shadow_record.has_intersection) && (t * t < light_distance_squared), BV/Renderer.cpp:195
+                if (t * t < d2) { occluded = true; return true; }
+            } else if (t <= best) {
+                best = t; best_tri = tri;   // (left.t < right.t) ? left : right: the later leaf wins ties
             }
         }
-        i = (hit && tri < 0) ? i + 1 : skip;
-    }
+        return false;
+    };
+    auto walk = [&](auto kind) {
+        constexpr bool FIN = decltype(kind)::value;
+        uint32_t i = 0;
+        while (i < n) {
+            const float bound = shadow ? sbound : ((best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff());
+            int p0 = -1, p1 = -1;
+            for (uint32_t s = 0; s < RT_WH_STEPS && i < n; ++s) {
+                const float4 q0 = nodes[2 * i];
+                const float4 q1 = nodes[2 * i + 1];
+                if (COUNT) ++node_tests;
+                const bool hit = FIN ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound) : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                const int tri = f2i(q1.w);
+                i = (hit && tri < 0) ? i + 1 : (uint32_t)f2i(q1.z);
+                if (hit && tri >= 0) {
+                    if (p0 < 0) p0 = tri;
+                    else { p1 = tri; break; }
+                }
+            }
+            // the postponed leaves in DFS order (the later leaf still wins ties)
+            if (p0 >= 0 && tri_test(p0)) return;
+            if (p1 >= 0 && tri_test(p1)) return;
+        }
+    };
+    if (rcp_finite(r)) walk(FiniteSlab{});
+    else walk(GeneralSlab{});
 }
 
 }  // namespace
 
+// frame groups per block: an 8x8 tile per block, wave g rendering the frames k = g (mod 4) of it; the
+// colors meet in LDS and wave 0 accumulates them in frame order (the reference's additions in its
+// order).  Against one thread per pixel rendering every frame (16x16 tiles), the blocks are 4x as many
+// at a quarter of the duration, so the last round of blocks leaves little of the chip idle, and a wave's
+// rays come from an 8x8 tile instead of a 16x4 strip: C3 6151 -> 9759 Msamples/s, bitwise
+// (profiles/r03/ab/ab_c3_whitted.json)
+constexpr uint32_t WH_FG = 4;
+
+// one frame of one pixel: Renderer::RayGen_Shader -> cast_Whitted_ray (BV/Renderer.cpp:109-233)
 template <bool COUNT>
-__global__ void __launch_bounds__(256) whitted_kernel(KParams P)
+__device__ __forceinline__ V3 whitted_sample(const KParams& P, uint32_t lx, uint32_t y, float cam_x, uint32_t& node_tests, uint32_t& tri_tests, uint32_t& rays)
 {
-    const uint32_t tiles_x = (P.W + 15) / 16;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t lr = (tile / tiles_x) * 16 + (threadIdx.x >> 4);
-    const uint32_t lx = (tile % tiles_x) * 16 + (threadIdx.x & 15);
-    uint32_t node_tests = 0, tri_tests = 0, rays = 0;
-    if (lr < P.n_local_rows && lx < P.W) {
-        const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
-        const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
-        const uint32_t local = lr * P.W + lx;
-        float4 acc = (P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[local];
-        float cam_x = P.cam_pos[0];
-        for (uint32_t k = 0; k < P.n_frames; ++k) {
-            // the reference evaluates every frame; keep the compiler from hoisting the frame's work
-            asm volatile("" : "+v"(cam_x));
-            // Camera::RecomputeRayDirections, BV/Camera.cpp:119-129: bottom-left corner of the pixel
-            float cx = (float)lx / (float)P.W;
-            float cy = (float)y / (float)P.H;
-            cx = cx * 2.0f - 1.0f;
-            cy = cy * 2.0f - 1.0f;
-            float tg[4];
-            mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(divs(V3{tg[0], tg[1], tg[2]}, tg[3]));
-            float wd[4];
-            mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
-            const V3 cam{cam_x, P.cam_pos[1], P.cam_pos[2]};
-            const Ray ray = make_ray(cam, w_normalize(V3{wd[0], wd[1], wd[2]}));   // RayGen_Shader, BV/Renderer.cpp:113
-            V3 color{P.sky[0], P.sky[1], P.sky[2]};
-            double best = 1.7976931348623157e308;
-            int best_tri = -1;
-            bool occl = false;
-            if (ray.d.x == 0.0f && ray.d.y == 0.0f && ray.d.z == 0.0f) {
-                color = V3{0.0f, 0.0f, 0.0f};   // zero direction: no energy (BV/Renderer.cpp:123-126)
-            } else {
-                if (COUNT) ++rays;
-                whitted_traverse<COUNT>(P, ray, false, 0.0, best, best_tri, occl, node_tests, tri_tests);
-            }
-            if (best_tri >= 0) {
-                const float4 ta = P.tris[4 * best_tri], tn = P.tris[4 * best_tri + 3];
-                const int mat = f2i(ta.w);
-                const V3 x = add(ray.o, smul((float)best, ray.d));   // Ray::operator(), BV/Ray.h:34-37
-                const V3 n{tn.x, tn.y, tn.z};
-                const V3 off = muls(n, INTERSECTION_CORRECTION);
-                const V3 sp = (dot(ray.d, n) < 0.0f) ? add(x, off) : sub(x, off);
-                V3 diffuse{0.0f, 0.0f, 0.0f};
-                for (uint32_t l = 0; l < P.n_plights; ++l) {
-                    const float4 lp = P.plights[2 * l], lr4 = P.plights[2 * l + 1];
-                    V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
-                    const float d2 = dot(ld, ld);
-                    ld = w_normalize(ld);
-                    const Ray sray = make_ray(sp, ld);
-                    if (COUNT) ++rays;
-                    double sbest = 1.7976931348623157e308;
-                    int stri = -1;
-                    bool blocked = false;
-                    whitted_traverse<COUNT>(P, sray, true, (double)d2, sbest, stri, blocked, node_tests, tri_tests);
-                    if (blocked) continue;
-                    const float c = __builtin_fabsf(dot(ld, n));
-                    diffuse = add(diffuse, V3{lr4.x * c, lr4.y * c, lr4.z * c});
-                }
-                const float4 wm = P.wmats[mat];
-                color = muls(mul(diffuse, V3{wm.x, wm.y, wm.z}), wm.w);
-            }
-            acc.x = acc.x + color.x; acc.y = acc.y + color.y; acc.z = acc.z + color.z; acc.w = acc.w + 1.0f;
-        }
-        if (P.n_frames > 0) {
-            const float fr = (float)(P.first_frame + P.n_frames - 1u);
-            const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
-            const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
-            P.accum[local] = acc;
-            P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
-        }
+    // Camera::RecomputeRayDirections, BV/Camera.cpp:119-129: bottom-left corner of the pixel
+    float cx = (float)lx / (float)P.W;
+    float cy = (float)y / (float)P.H;
+    cx = cx * 2.0f - 1.0f;
+    cy = cy * 2.0f - 1.0f;
+    float tg[4];
+    mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
+    const V3 dv = glm_normalize(divs(V3{tg[0], tg[1], tg[2]}, tg[3]));
+    float wd[4];
+    mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
+    const V3 cam{cam_x, P.cam_pos[1], P.cam_pos[2]};
+    const Ray ray = make_ray(cam, w_normalize(V3{wd[0], wd[1], wd[2]}));   // RayGen_Shader, BV/Renderer.cpp:113
+    V3 color{P.sky[0], P.sky[1], P.sky[2]};
+    double best = 1.7976931348623157e308;
+    int best_tri = -1;
+    bool occl = false;
+    if (ray.d.x == 0.0f && ray.d.y == 0.0f && ray.d.z == 0.0f) {
+        color = V3{0.0f, 0.0f, 0.0f};   // zero direction: no energy (BV/Renderer.cpp:123-126)
+    } else {
+        if (COUNT) ++rays;
+        whitted_traverse<COUNT>(P, ray, false, 0.0, best, best_tri, occl, node_tests, tri_tests);
     }
+    if (best_tri >= 0) {
+        const float4 ta = P.tris[4 * best_tri], tn = P.tris[4 * best_tri + 3];
+        const int mat = f2i(ta.w);
+        const V3 x = add(ray.o, smul((float)best, ray.d));   // Ray::operator(), BV/Ray.h:34-37
+        const V3 n{tn.x, tn.y, tn.z};
+        const V3 off = muls(n, INTERSECTION_CORRECTION);
+        const V3 sp = (dot(ray.d, n) < 0.0f) ? add(x, off) : sub(x, off);
+        V3 diffuse{0.0f, 0.0f, 0.0f};
+        for (uint32_t l = 0; l < P.n_plights; ++l) {
+            const float4 lp = P.plights[2 * l], lr4 = P.plights[2 * l + 1];
+            V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
+            const float d2 = dot(ld, ld);
+            ld = w_normalize(ld);
+            const Ray sray = make_ray(sp, ld);
+            if (COUNT) ++rays;
+            double sbest = 1.7976931348623157e308;
+            int stri = -1;
+            bool blocked = false;
+            whitted_traverse<COUNT>(P, sray, true, (double)d2, sbest, stri, blocked, node_tests, tri_tests);
+            if (blocked) continue;
+            const float c = __builtin_fabsf(dot(ld, n));
+            diffuse = add(diffuse, V3{lr4.x * c, lr4.y * c, lr4.z * c});
+        }
+        const float4 wm = P.wmats[mat];
+        color = muls(mul(diffuse, V3{wm.x, wm.y, wm.z}), wm.w);
+    }
+    return color;
+}
+
+__device__ __forceinline__ void whitted_store(const KParams& P, uint32_t local, const float4 acc)
+{
+    const float fr = (float)(P.first_frame + P.n_frames - 1u);
+    const float rx = smin(smax(acc.x / fr, 0.0f), 1.0f), gy = smin(smax(acc.y / fr, 0.0f), 1.0f);
+    const float bz = smin(smax(acc.z / fr, 0.0f), 1.0f), aw = smin(smax(acc.w / fr, 0.0f), 1.0f);
+    P.accum[local] = acc;
+    P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
+}
+
+template <bool COUNT>
+__global__ void __launch_bounds__(256, 8) whitted_kernel(KParams P)
+{
+    uint32_t node_tests = 0, tri_tests = 0, rays = 0;
+    constexpr uint32_t FG = WH_FG;
+    static_assert(FG * 64 == 256, "one wave per frame group");
+    __shared__ float4 col[2][FG][64];   // the step's colors, double-buffered (one barrier per step)
+    const uint32_t tiles_x = (P.W + 7) / 8;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t p = threadIdx.x & 63u, g = threadIdx.x >> 6;
+    const uint32_t lr = (tile / tiles_x) * 8 + (p >> 3);
+    const uint32_t lx = (tile % tiles_x) * 8 + (p & 7u);
+    const bool valid = lr < P.n_local_rows && lx < P.W;
+    const uint32_t band_k = lr / P.band, in_band = lr - band_k * P.band;
+    const uint32_t y = (P.rank + band_k * P.nranks) * P.band + in_band;
+    const uint32_t local = lr * P.W + lx;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g == 0 && valid && P.first_frame != 1u) acc = P.accum[local];
+    float cam_x = P.cam_pos[0];
+    const uint32_t nsteps = (P.n_frames + FG - 1u) / FG;
+    for (uint32_t j = 0; j < nsteps; ++j) {
+        // the reference evaluates every frame; keep the compiler from hoisting the frame's work
+        asm volatile("" : "+v"(cam_x));
+        const uint32_t k = j * FG + g;
+        if (valid && k < P.n_frames) {
+            const V3 c = whitted_sample<COUNT>(P, lx, y, cam_x, node_tests, tri_tests, rays);
+            col[j & 1u][g][p] = make_float4(c.x, c.y, c.z, 0.0f);
+        }
+        __syncthreads();
+        if (g == 0 && valid) {
+            // frames j*FG .. j*FG+FG-1 in order (RayGen_Shader's accumulation)
+            for (uint32_t u = 0; u < FG && j * FG + u < P.n_frames; ++u) {
+                const float4 c = col[j & 1u][u][p];
+                acc.x = acc.x + c.x; acc.y = acc.y + c.y; acc.z = acc.z + c.z; acc.w = acc.w + 1.0f;
+            }
+        }
+        // buffer j & 1 is written again at step j + 2, after the barrier of step j + 1, which wave 0
+        // reaches only when this chain is done
+    }
+    if (g == 0 && valid && P.n_frames > 0) whitted_store(P, local, acc);
     if (COUNT) {
         uint64_t a = node_tests, b = tri_tests, c = rays;
         for (int off = 32; off > 0; off >>= 1) {
@@ -150,7 +221,7 @@ __global__ void __launch_bounds__(256) whitted_kernel(KParams P)
 
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out)
 {
-    const uint32_t tiles = ((P.W + 15) / 16) * ((P.n_local_rows + 15) / 16);
+    const uint32_t tiles = ((P.W + 7) / 8) * ((P.n_local_rows + 7) / 8);
     if (grid_out) *grid_out = tiles;
     if (tiles == 0) return hipSuccess;
     if (count) hipLaunchKernelGGL(whitted_kernel<true>, dim3(tiles), dim3(256), 0, stream, P);
@@ -443,7 +514,7 @@ __global__ void __launch_bounds__(256) whitted_world_kernel(KParams P)
 
 hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out)
 {
-    const uint32_t tiles = ((P.W + 15) / 16) * ((P.n_local_rows + 15) / 16);
+    const uint32_t tiles = ((P.W + 7) / 8) * ((P.n_local_rows + 7) / 8);
     if (grid_out) *grid_out = tiles;
     if (tiles == 0) return hipSuccess;
     if (P.max_bounce_depth + 2 > kWorldFrames) return hipErrorInvalidValue;   // the explicit stack bounds the recursion

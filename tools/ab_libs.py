@@ -31,30 +31,34 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--fast", action="store_true")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3"])
     args = ap.parse_args()
     W, H, spp = args.width, args.height, args.spp
     runs = {}
     for name in args.libs:
         rt = load(name)
+        bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
         if args.scene == "c5":
-            sc = rt.Scene.cornell_c5(np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"])
+            sc = rt.Scene.cornell_c5(bvh["raw_bunny"])
+        elif args.scene == "c3":   # Whitted bunny + teapot (C3: 1280x960x64)
+            sc = rt.Scene.bvh_tracer(bvh["raw_bunny"], bvh["raw_teapot"])
         else:
             sc = rt.Scene.cornell()
         ctx = rt.Context(0)
         ctx.upload(sc)
         ctx.resize(W, H)
-        cam, _, _ = rt.camera_default(W, H)
+        cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else rt.camera_default(W, H)[0]
         runs[name] = (rt, ctx, cam, [], sc)
+    kw = dict(whitted=True) if args.scene == "c3" else dict(exact=not args.fast)
     ref = None
     for r in range(args.rounds + 1):
         for name, (rt, ctx, cam, res, _) in runs.items():
-            ctx.render(cam, spp, fetch=False, exact=not args.fast)
+            ctx.render(cam, spp, fetch=False, **kw)
             if r > 0:
                 res.append(W * H * spp / ctx.stats().last_kernel_ms / 1e3)
     out = {}
     for name, (rt, ctx, cam, res, _) in runs.items():
-        _, acc = ctx.render(cam, 4, exact=not args.fast)
+        _, acc = ctx.render(cam, 4, **kw)
         same = None if ref is None else bool(np.array_equal(acc.view(np.uint32), ref.view(np.uint32)))
         ref = acc if ref is None else ref
         out[name] = {"median_msps": round(float(np.median(res)), 1), "grid": ctx.stats().grid, "bitwise_equal_to_first": same}
