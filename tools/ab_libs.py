@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--fast", action="store_true")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3", "c1"])
     args = ap.parse_args()
     W, H, spp = args.width, args.height, args.spp
     runs = {}
@@ -40,6 +40,8 @@ def main():
         bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
         if args.scene == "c5":
             sc = rt.Scene.cornell_c5(bvh["raw_bunny"])
+        elif args.scene == "c1":   # Whitted two spheres (C1: 640x480x1)
+            sc = rt.Scene.two_spheres()
         elif args.scene == "c3":   # Whitted bunny + teapot (C3: 1280x960x64)
             sc = rt.Scene.bvh_tracer(bvh["raw_bunny"], bvh["raw_teapot"])
         else:
@@ -47,9 +49,9 @@ def main():
         ctx = rt.Context(0)
         ctx.upload(sc)
         ctx.resize(W, H)
-        cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else rt.camera_default(W, H)[0]
+        cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else (rt.camera_two_spheres(W, H) if args.scene == "c1" else rt.camera_default(W, H)[0])
         runs[name] = (rt, ctx, cam, [], sc)
-    kw = dict(whitted=True) if args.scene == "c3" else dict(exact=not args.fast)
+    kw = dict(whitted=True) if args.scene in ("c1", "c3") else dict(exact=not args.fast)
     ref = None
     for r in range(args.rounds + 1):
         for name, (rt, ctx, cam, res, _) in runs.items():
