@@ -105,6 +105,7 @@ struct rt_ctx {
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
+    bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
@@ -404,6 +405,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
@@ -829,11 +831,18 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
                     uint32_t lf = 0;
                     while ((1u << lf) < nf && lf < 6) ++lf;
-                    // a wave of the path kernel takes whole segments: keep at least 32 per wave, so the
-                    // launch's tail (the waves' last segments) stays short when a pass has few tiles (a
-                    // rank's row bands of a multi-GPU frame: 8 ranks at C4 -> 16-frame segments)
+                    // a wave of the path kernel takes parts of segments: keep at least 32 parts per wave, so
+                    // the launch's tail (the waves' last parts) stays short when a pass has few tiles (a rank's
+                    // row bands of a multi-GPU frame).  The segments stay long (the pre-pass's per-segment
+                    // work -- the tile's box list, the record counter -- is paid once per 64 frames) and the
+                    // path kernel splits each into 2^ps parts of its records, as fine as 8 frames' worth
+                    // (8 ranks at C4: 8 parts of 64-frame segments; one-segment-per-part with 8-frame
+                    // segments cost the pre-pass 0.9 ms more, profiles/r03/numbers/band_split*.jsonl)
                     const uint64_t waves = (uint64_t)grid * (c->block / 64u);
-                    while (lf > 3 && (uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) < 32u * waves) --lf;
+                    uint32_t ps = 0;
+                    while (lf - ps > 3 && ((uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) << ps) < 32u * waves) ++ps;
+                    if (c->seg_parts_off) { lf -= ps; ps = 0; }   // A/B: short segments, one part each
+                    Q.seg_part_shift = ps;
                     Q.seg_frames = 1u << lf;
                     Q.seg_shift = 6 + lf;
                     const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);

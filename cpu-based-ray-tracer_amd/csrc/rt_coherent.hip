@@ -387,7 +387,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
     uint32_t seg_pos = 0, seg_end = 0;
-    const uint32_t n_list = PRE ? __builtin_amdgcn_readfirstlane(*P.seg_list_n) : 0u;
+    const uint32_t n_list = PRE ? __builtin_amdgcn_readfirstlane(*P.seg_list_n) << P.seg_part_shift : 0u;
     bool list_left = true;
 
 #if RT_SECTIONS
@@ -424,9 +424,12 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
                 k = __builtin_amdgcn_readfirstlane(k);
                 if (k >= n_list) { list_left = false; break; }
-                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k]);
-                seg_pos = sg << Q.seg_shift;
-                seg_end = seg_pos + __builtin_amdgcn_readfirstlane(Q.ccount[sg]);
+                // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records
+                const uint32_t ps = Q.seg_part_shift, part = k & ((1u << ps) - 1u);
+                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k >> ps]);
+                const uint32_t cnt = __builtin_amdgcn_readfirstlane(Q.ccount[sg]);
+                seg_pos = (sg << Q.seg_shift) + ((part * cnt) >> ps);
+                seg_end = (sg << Q.seg_shift) + (((part + 1u) * cnt) >> ps);
                 continue;
             }
             const uint32_t avail = seg_end - seg_pos;

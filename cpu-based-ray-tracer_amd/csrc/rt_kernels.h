@@ -61,10 +61,12 @@ struct KParams {
     // 8x8 tile x seg_frames (a power of two <= 64) frames, segment s = chunk * n_tiles + tile (chunk-major);
     // the surface hits of segment s are records [s << seg_shift, + ccount[s]) of crec: (location.xyz, tag),
     // tag = triangle | pixel-in-tile << 19 | frame-in-chunk << 25 | flipped normal << 31; the non-empty
-    // segments are listed in seg_list[0, *seg_list_n) (misses and light hits are parked by the pre-pass)
+    // segments are listed in seg_list[0, *seg_list_n) (misses and light hits are parked by the pre-pass);
+    // the path kernel takes each listed segment in 2^seg_part_shift parts (consecutive record ranges), so a
+    // pass with few tiles keeps long pre-pass segments and still hands out fine-grained work
     float4* crec; uint32_t* ccount; uint32_t* seg_list; uint32_t* seg_list_n;
     unsigned long long* tile_boxes;   // per tile: the leaf boxes its camera rays' frustum meets (tile_boxes_kernel)
-    uint32_t n_segments, n_tiles, seg_frames, seg_shift;
+    uint32_t n_segments, n_tiles, seg_frames, seg_shift, seg_part_shift;
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray

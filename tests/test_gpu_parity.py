@@ -207,16 +207,29 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
         assert np.array_equal(bits(out[k][1]), bits(out["1"][1]))
     monkeypatch.delenv("RT_VERTEX")
     monkeypatch.delenv("RT_CHUNKS")
-    # the vertex kernel: its camera pre-pass groups a tile's frames in segments of 8-64 frames (the
-    # smaller, the fewer tiles a pass has: here 8, so 70 frames take 9 segments per tile, the last of 6)
+    # the vertex kernel: its camera pre-pass groups a tile's frames in segments of up to 64 frames (70
+    # frames: 2 segments per tile, the last of 6), and the path kernel takes each segment in up to 8 parts
+    # when a pass has few tiles (here 8).  RT_SEG_PARTS_OFF=1 shortens the segments instead (8 frames: 9
+    # segments per tile, the last of 6, one part each); both give the megakernel's bits
     c = rt.Context(0)
     try:
         c.upload(rt.Scene.cornell())
         c.resize(W, H)
         _, v = c.render(cam, 70, seed=3)
+        assert c.stats().kernel == 1 and c.stats().n_chunks == 2
+    finally:
+        c.close()
+    monkeypatch.setenv("RT_SEG_PARTS_OFF", "1")
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        _, v8 = c.render(cam, 70, seed=3)
         assert c.stats().kernel == 1 and c.stats().n_chunks == 9
     finally:
         c.close()
+    monkeypatch.delenv("RT_SEG_PARTS_OFF")
+    assert np.array_equal(bits(v8), bits(v))
     monkeypatch.setenv("RT_VERTEX", "0")
     c = rt.Context(0)
     try:
