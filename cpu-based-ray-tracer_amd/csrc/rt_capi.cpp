@@ -32,6 +32,9 @@ struct rt_ctx {
     std::string err;
     // scene
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr, *d_lboxes = nullptr;
+    float4* d_sboxes = nullptr;   // split trace (FlatScene::sboxes): outside leaf boxes
+    int32_t* d_stri = nullptr;    // split trace: outside slot -> triangle
+    uint32_t split_root = 0, split_end = 0, n_sboxes = 0;
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
     bool qbvh = false;                             // RT_QBVH=1: the BVH variant walks the compact BVH (A/B: slower)
@@ -105,11 +108,16 @@ struct rt_ctx {
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
+    bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
     uint32_t vthresh = 32, vsteps = 8; // the same for the vertex kernel's BVH variant (C5 sweep)
+    uint32_t sthresh = 8, ssteps = 12; // the BVH variant with the split trace: few lanes walk, so rounds run while
+                                       // more than 8 of them do (C5 sweep 2 / 4 / 6 / 8 / 12 / 16 / 32: 3003 / 3283 /
+                                       // 3399 / 3419-3427 / 3403 / 3261 / 2588 Msamples/s), 12 box tests per round
+                                       // (4 / 8 / 12 / 16: 3336 / 3427 / 3466 / 3461; profiles/r03/ab/ab_c5_split.json)
 };
 
 namespace {
@@ -400,11 +408,12 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     rt_ctx* c = new (std::nothrow) rt_ctx;
     if (!c) return RT_ERR_OOM;
     c->device = cfg ? cfg->device : 0;
-    if (const char* e = std::getenv("RT_THRESH")) c->thresh = c->vthresh = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_STEPS")) c->steps = c->vsteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = std::getenv("RT_THRESH")) c->thresh = c->vthresh = c->sthresh = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = std::getenv("RT_STEPS")) c->steps = c->vsteps = c->ssteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = std::getenv("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = std::getenv("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
@@ -469,6 +478,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    dfree(c->d_sboxes); dfree(c->d_stri);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_lboxes); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
     dfree(c->d_went); dfree(c->d_wtris);
@@ -502,6 +512,11 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_lnodes, s->flat.lnodes)) != RT_OK) return r;
     if ((r = upload(c, c->d_ltris, s->flat.ltris)) != RT_OK) return r;
     if ((r = upload(c, c->d_lboxes, s->flat.lboxes)) != RT_OK) return r;
+    if ((r = upload(c, c->d_sboxes, s->flat.sboxes)) != RT_OK) return r;
+    if ((r = upload(c, c->d_stri, s->flat.stri)) != RT_OK) return r;
+    c->split_root = s->flat.split_root;
+    c->split_end = s->flat.split_end;
+    c->n_sboxes = (uint32_t)(s->flat.sboxes.size() / 8);
     if ((r = upload(c, c->d_qnodes, s->flat.qnodes)) != RT_OK) return r;
     if ((r = upload(c, c->d_tabc, s->flat.tabc)) != RT_OK) return r;
     if ((r = upload(c, c->d_tnrm, s->flat.tnrm)) != RT_OK) return r;
@@ -581,6 +596,8 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     c->d_nodes = d_nodes; c->d_tris = d_tris;
     // the BVH-walking kernels: no leaf-box table, no compact tree
     dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
+    dfree(c->d_sboxes); dfree(c->d_stri);   // the split refers to the host tree's node order
+    c->split_root = c->split_end = c->n_sboxes = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
     c->hdr.has_qnodes = 0;
@@ -655,6 +672,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.lnodes = c->d_lnodes; P.n_lnodes = c->hdr.n_lnodes;
     P.ltris = c->d_ltris; P.n_ltris = c->hdr.n_ltris;
     P.lboxes = c->d_lboxes; P.n_lboxes = c->brute ? c->hdr.n_lboxes : 0;
+    if (c->split && c->split_root != 0 && P.n_lboxes == 0) {
+        P.sboxes = c->d_sboxes; P.stri = c->d_stri; P.n_sboxes = c->n_sboxes;
+        P.split_root = c->split_root; P.split_end = c->split_end;
+    }
     P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
     P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;
     std::memcpy(P.q_origin, c->hdr.q_origin, sizeof P.q_origin);
@@ -723,7 +744,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         const uint32_t small = 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris;
         P.lds_scene_quads = (c->bvh_small_lds && small <= 64u) ? small : 0u;
         P.ring_pack = (c->ring_pack >= 1 && c->hdr.n_mats <= 8) ? 1u : 0u;
-        P.thresh = c->vthresh; P.steps = c->vsteps;
+        P.thresh = P.split_root != 0u ? c->sthresh : c->vthresh;
+        P.steps = P.split_root != 0u ? c->ssteps : c->vsteps;
     }
     if (coh_box && exact) P.ring_pack = (c->ring_pack >= 2 && c->hdr.n_mats <= 8) ? 1u : 0u;
     // EXACT: as many fold-stack levels in LDS as fit beside the scene without costing occupancy

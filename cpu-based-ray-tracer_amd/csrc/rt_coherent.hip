@@ -382,7 +382,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
     if (EXACT) lsu(VS_BASE) = 0u;
     // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
-    const uint32_t NN = S.n_nodes;
+    // (split trace: the walk stays inside the subtree [split_root, split_end), NN = split_end marks a done ray)
+    const uint32_t NN = (BVH && P.split_root != 0u) ? P.split_end : S.n_nodes;
     uint32_t tiA = NN, tiB = NN;
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
@@ -990,6 +991,77 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             // trace or nobody waits for service.
             CKParams& Q = kargs4();
             const uint32_t thresh = Q.thresh, steps = Q.steps;
+            if (Q.split_root != 0u) {
+                // Split trace (rt_scene.cpp): a fresh ray (ti == 0) first tests the <= 64 leaves outside the
+                // walked subtree by their own boxes -- one wave-uniform loop of scalar box loads, the
+                // leaf-box variant's trace -- and the subtree's root box; it walks the subtree only when that
+                // box is hit (entered within the bound).  Every ancestor box contains these boxes and the
+                // finite slab test is monotone, so a box's own test decides whether the reference reaches it.
+                // The closest hit is taken by (min t, max triangle) -- triangles are numbered in DFS order --
+                // since the outside leaves are tested before the subtree's; a ray with a non-finite reciprocal
+                // walks the whole tree on its own lane (the reference's traversal).
+                // one ray at a time (A, then B): the box loop and the candidates of one ray live at once
+#pragma nounroll
+                for (uint32_t k = 0; k < 2u; ++k) {
+                    const bool isA = k == 0u;
+                    const bool fresh = in_path && (isA ? tiA : tiB) == 0u && !(!isA && occB);
+                    if (!__any(fresh)) continue;
+                    const V3 d = isA ? dA : dB;
+                    const Ray r{o, d, rcp3(d), d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
+                    const bool fin = finite3(r.rcp) && Q.force_walk == 0u;
+                    // ray A: no bound yet (its first candidates); ray B: no blocker beyond the light point
+                    const float bnd = isA ? __builtin_inff() : slen * 1.00001f + 1e-5f;
+                    uint64_t cm = 0;
+                    {
+                        cbox8* bx = (cbox8*)kargs4().sboxes;
+                        const uint32_t nb = kargs4().n_sboxes;
+                        for (uint32_t b = 0; b < nb; ++b) {
+                            const box8 q = bx[b];
+                            const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
+                            const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
+                            const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
+                            const uint64_t m = (uint64_t)(uint32_t)f2i(q.s6) | ((uint64_t)(uint32_t)f2i(q.s7) << 32);
+                            cm |= box_hit_pk_within(sx, sy, sz, r.rcp, bnd) ? m : 0ull;
+                        }
+                    }
+                    if (!(fresh && fin)) cm = 0;
+                    while (cm != 0) {
+                        const int tri = kargs4().stri[__builtin_ctzll(cm)];
+                        cm &= cm - 1;
+                        const float4* T = S.tris + 4 * tri;
+                        const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+                        double t;
+                        if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                            if (isA) {
+                                if (t < tA || (t == tA && tri > triA)) { tA = t; triA = tri; }
+                            } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
+                                occB = true;
+                                cm = 0;
+                            }
+                        }
+                    }
+                    if (fresh) {
+                        uint32_t ti = NN;
+                        if (fin) {
+                            const uint32_t root = kargs4().split_root;
+                            const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
+                            const float bound = isA ? ((tA < 1e30) ? (float)tA * 1.00001f + 1e-5f : __builtin_inff()) : bnd;
+                            if (!(!isA && occB) && slab_hit_finite_within(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, bound)) ti = root;
+                        } else {
+                            // the reference's traversal of the whole tree on this lane
+                            SceneView W = S;
+                            W.n_nodes = kargs4().n_nodes;
+                            uint32_t nt = 0, tt = 0;
+                            double db = 1.7976931348623157e308;
+                            int dt = -1;
+                            bool dummy = false;
+                            traverse_impl<false, false>(W, r, !isA, (double)slen, isA ? tA : db, isA ? triA : dt, isA ? dummy : occB, nt, tt);
+                        }
+                        if (isA) tiA = ti;
+                        else tiB = ti;
+                    }
+                }
+            }
             for (;;) {
                 const bool tracing = in_path && (tiA < NN || tiB < NN);
                 const uint64_t act = __ballot(tracing);
@@ -1083,7 +1155,9 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         double t;
                         if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {
-                                if (t <= tA) { tA = t; triA = pk; }   // the later leaf wins ties
+                                // the later leaf wins ties (MC/BVH.h:97-100): triangles are numbered in DFS order,
+                                // and the split trace's outside leaves are tested first
+                                if (t < tA || (t == tA && pk > triA)) { tA = t; triA = pk; }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 ti = NN;

@@ -440,6 +440,63 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             }
         }
     }
+    // ---- split trace of a larger scene: the deepest internal node whose subtree leaves at most 64 leaves
+    // outside it (the subtrees with that property form the chain from the root down to it).  The outside
+    // leaves are tested by their own boxes, exactly as the small scenes' leaf boxes above (every ancestor
+    // box must contain the leaf box), and the subtree is walked from its root, whose box must likewise lie
+    // inside every ancestor's: then the root's own slab test decides whether the reference enters it.
+    out.sboxes.clear();
+    out.stri.clear();
+    out.split_root = out.split_end = 0;
+    if (NT > 64) {
+        std::vector<uint32_t> leaf_pre(NN + 1, 0);   // leaves among nodes [0, i)
+        for (uint32_t i = 0; i < NN; ++i) leaf_pre[i + 1] = leaf_pre[i] + (fn[i].tri >= 0 ? 1u : 0u);
+        const uint32_t n_leaves = leaf_pre[NN];
+        uint32_t r = 0;
+        for (uint32_t i = 1; i < NN; ++i) {
+            if (fn[i].tri >= 0) continue;
+            const uint32_t end = (uint32_t)fn[i].skip;
+            const uint32_t outside = n_leaves - (leaf_pre[end] - leaf_pre[i]);
+            if (outside <= 64 && (r == 0 || end - i < (uint32_t)fn[r].skip - r)) r = i;
+        }
+        auto inside_ancestors = [&](uint32_t i) {   // every ancestor box of node i contains its box
+            const Box& lb = fn[i].box;
+            for (uint32_t j = 0; j < i; ++j) {
+                if (fn[j].tri >= 0 || fn[j].skip <= (int)i) continue;   // not an ancestor of node i
+                const Box& ab = fn[j].box;
+                if (!(ab.lo.x <= lb.lo.x && ab.lo.y <= lb.lo.y && ab.lo.z <= lb.lo.z && ab.hi.x >= lb.hi.x && ab.hi.y >= lb.hi.y &&
+                      ab.hi.z >= lb.hi.z)) return false;
+            }
+            return true;
+        };
+        const uint32_t rend = r ? (uint32_t)fn[r].skip : 0u;
+        bool ok = r != 0 && inside_ancestors(r);
+        std::vector<std::pair<Box, uint64_t>> uniq;
+        std::vector<int32_t> slots;
+        for (uint32_t i = 0; i < NN && ok; ++i) {
+            if (fn[i].tri < 0 || (i >= r && i < rend)) continue;
+            if (!inside_ancestors(i)) { ok = false; break; }
+            const Box& lb = fn[i].box;
+            size_t k = 0;
+            while (k < uniq.size() && std::memcmp(&uniq[k].first, &lb, sizeof(Box)) != 0) ++k;
+            if (k == uniq.size()) uniq.emplace_back(lb, 0ull);
+            uniq[k].second |= 1ull << slots.size();
+            slots.push_back(fn[i].tri);
+        }
+        if (ok && !slots.empty()) {
+            out.split_root = r;
+            out.split_end = rend;
+            out.stri = slots;
+            out.sboxes.resize(uniq.size() * 8);
+            for (size_t k = 0; k < uniq.size(); ++k) {
+                const Box& b = uniq[k].first;
+                float* q = &out.sboxes[8 * k];
+                q[0] = b.lo.x; q[1] = b.hi.x; q[2] = b.lo.y; q[3] = b.hi.y;
+                q[4] = b.lo.z; q[5] = b.hi.z;
+                q[6] = bits_as_float((int32_t)(uint32_t)uniq[k].second); q[7] = bits_as_float((int32_t)(uint32_t)(uniq[k].second >> 32));
+            }
+        }
+    }
     out.tris.resize((size_t)NT * 16);
     out.dbg_tri_f.resize((size_t)NT * 13);
     out.dbg_tri_i.resize((size_t)NT * 2);

@@ -48,6 +48,13 @@ struct FlatScene {
     std::vector<float> nodes, tris, mats, lnodes, ltris, wmats, plights;   // float4-granular
     std::vector<float> went, wtris;                                       // Whitted world (C1)
     std::vector<float> lboxes;                                            // distinct leaf boxes (small scenes)
+    // split trace (larger scenes, the vertex kernel's BVH variant): the subtree [split_root, split_end) of
+    // the DFS pre-order is walked; the <= 64 leaves outside it are tested by their distinct leaf boxes
+    // (sboxes: the lboxes layout, the masks over outside slots), slot k = the k-th outside leaf in DFS
+    // order = triangle stri[k]; split_root = 0: no split
+    std::vector<float> sboxes;
+    std::vector<int32_t> stri;
+    uint32_t split_root = 0, split_end = 0;
     std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
     std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag

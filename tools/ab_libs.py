@@ -35,7 +35,12 @@ def main():
     args = ap.parse_args()
     W, H, spp = args.width, args.height, args.spp
     runs = {}
-    for name in args.libs:
+    for spec in args.libs:
+        # "lib.so:K=V,K=V": environment knobs read at this library's context creation (rt_create)
+        name, _, env = spec.partition(":")
+        kv = [e.split("=", 1) for e in env.split(",") if e]
+        for k, v in kv:
+            os.environ[k] = v
         rt = load(name)
         bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
         if args.scene == "c5":
@@ -50,7 +55,9 @@ def main():
         ctx.upload(sc)
         ctx.resize(W, H)
         cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else (rt.camera_two_spheres(W, H) if args.scene == "c1" else rt.camera_default(W, H)[0])
-        runs[name] = (rt, ctx, cam, [], sc)
+        for k, _ in kv:
+            os.environ.pop(k, None)
+        runs[spec] = (rt, ctx, cam, [], sc)
     kw = dict(whitted=True) if args.scene in ("c1", "c3") else dict(exact=not args.fast)
     ref = None
     for r in range(args.rounds + 1):
