@@ -382,8 +382,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     uint32_t dleft = 0;                       // levels of the draining fold still to apply
     if (EXACT) lsu(VS_BASE) = 0u;
     // BVH: next node of ray A / ray B (NN: no ray or done); the traversal spans iterations
-    // (split trace: the walk stays inside the subtree [split_root, split_end), NN = split_end marks a done ray)
-    const uint32_t NN = (BVH && P.split_root != 0u) ? P.split_end : S.n_nodes;
+    const uint32_t NN = S.n_nodes;
     uint32_t tiA = NN, tiB = NN;
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
@@ -998,8 +997,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 // box is hit (entered within the bound).  Every ancestor box contains these boxes and the
                 // finite slab test is monotone, so a box's own test decides whether the reference reaches it.
                 // The closest hit is taken by (min t, max triangle) -- triangles are numbered in DFS order --
-                // since the outside leaves are tested before the subtree's; a ray with a non-finite reciprocal
-                // walks the whole tree on its own lane (the reference's traversal).
+                // since the outside leaves are tested before the subtree's.
                 // one ray at a time (A, then B): the box loop and the candidates of one ray live at once
 #pragma nounroll
                 for (uint32_t k = 0; k < 2u; ++k) {
@@ -1025,38 +1023,34 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         }
                     }
                     if (!(fresh && fin)) cm = 0;
+                    // the subtree's root box before the candidates (the reciprocals are then dead): for ray A
+                    // without a bound -- the walk's first step tests the root again under the closest outside
+                    // hit; ray B within the light distance.  A walk that leaves the subtree goes on through the
+                    // nodes after it (outside leaves, tested again: the same t and triangle change nothing).
+                    // A ray with a non-finite reciprocal keeps ti = 0 and walks the whole tree in the rounds
+                    // (the std::max/min slab test), like the whole-tree walk.
+                    uint32_t ti = NN;
+                    if (fresh && fin) {
+                        const uint32_t root = kargs4().split_root;
+                        const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
+                        if (slab_hit_finite_within(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, bnd)) ti = root;
+                    }
                     while (cm != 0) {
                         const int tri = kargs4().stri[__builtin_ctzll(cm)];
                         cm &= cm - 1;
-                        const float4* T = S.tris + 4 * tri;
-                        const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+                        const float* T = reinterpret_cast<const float*>(S.tris + 4 * tri);   // a, e1, e2 (xyz of 3 float4)
                         double t;
-                        if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t)) {
+                        if (moller_trumbore_od(V3{T[0], T[1], T[2]}, V3{T[4], T[5], T[6]}, V3{T[8], T[9], T[10]}, o, d, t)) {
                             if (isA) {
                                 if (t < tA || (t == tA && tri > triA)) { tA = t; triA = tri; }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 cm = 0;
+                                ti = NN;
                             }
                         }
                     }
-                    if (fresh) {
-                        uint32_t ti = NN;
-                        if (fin) {
-                            const uint32_t root = kargs4().split_root;
-                            const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
-                            const float bound = isA ? ((tA < 1e30) ? (float)tA * 1.00001f + 1e-5f : __builtin_inff()) : bnd;
-                            if (!(!isA && occB) && slab_hit_finite_within(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, bound)) ti = root;
-                        } else {
-                            // the reference's traversal of the whole tree on this lane
-                            SceneView W = S;
-                            W.n_nodes = kargs4().n_nodes;
-                            uint32_t nt = 0, tt = 0;
-                            double db = 1.7976931348623157e308;
-                            int dt = -1;
-                            bool dummy = false;
-                            traverse_impl<false, false>(W, r, !isA, (double)slen, isA ? tA : db, isA ? triA : dt, isA ? dummy : occB, nt, tt);
-                        }
+                    if (fresh && fin) {
                         if (isA) tiA = ti;
                         else tiB = ti;
                     }
