@@ -81,7 +81,8 @@ REFLECTIVE, REFLECTIVE_REFRACTIVE, DIFFUSE_GLOSSY = 0, 1, 2
 class SceneInfo(C.Structure):
     _fields_ = [("n_meshes", C.c_uint32), ("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_light_tris", C.c_uint32),
                 ("max_depth", C.c_uint32), ("light_mesh", C.c_int32), ("light_area", C.c_float), ("device_bytes", C.c_uint64),
-                ("n_leaf_boxes", C.c_uint32), ("n_light_skip", C.c_uint32)]
+                ("n_leaf_boxes", C.c_uint32), ("n_light_skip", C.c_uint32),
+                ("split_root", C.c_uint32), ("split_end", C.c_uint32), ("n_split_leaves", C.c_uint32), ("n_split_boxes", C.c_uint32)]
 
 
 def _fp(a):

@@ -386,6 +386,10 @@ rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
         skip += (uint32_t)__builtin_popcount(m);
     }
     info->n_light_skip = skip;
+    info->split_root = s->flat.split_root;
+    info->split_end = s->flat.split_end;
+    info->n_split_leaves = (uint32_t)s->flat.stri.size();
+    info->n_split_boxes = (uint32_t)(s->flat.sboxes.size() / 8);
     return RT_OK;
 }
 

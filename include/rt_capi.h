@@ -106,6 +106,11 @@ typedef struct {
     uint32_t n_leaf_boxes; /* distinct leaf boxes of a small scene's coherent trace (0: BVH traversal) */
     uint32_t n_light_skip; /* (light triangle, triangle) pairs whose shadow-ray candidates the vertex kernel skips
                               (near-coplanar with the light; 0 when the scene's error bound does not hold) */
+    uint32_t split_root;   /* split trace of a larger scene (the vertex kernel's BVH variant): the walked subtree
+                              [split_root, split_end) of the DFS pre-order; 0 when the scene has none */
+    uint32_t split_end;
+    uint32_t n_split_leaves;   /* leaves outside that subtree, tested by their boxes (<= 64) */
+    uint32_t n_split_boxes;    /* their distinct boxes */
 } rt_scene_info;
 rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 /* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node

@@ -75,6 +75,36 @@ def test_scene_build_matches_reference(scene, fixture):
     assert gg.scene_digest(nodes, tris) == str(fixture["digest"])
 
 
+def test_split_trace_tables(scene):
+    """The split trace's host tables (rt_scene.cpp): the walked subtree is the deepest one leaving at most
+    64 leaves outside it -- in C5 the bunny's mesh subtree, with the Cornell box's 32 triangles outside --
+    the outside leaves are exactly the leaves outside [split_root, split_end), every one inside all its
+    ancestor boxes, and the subtree's root box inside every ancestor's (leaf-box monotonicity)."""
+    info = scene.info()
+    nf, ni, tf, ti = scene.export()
+    r, e = info.split_root, info.split_end
+    assert r > 0 and e > r and info.n_split_leaves == 32 and 0 < info.n_split_boxes <= 32
+    leaf = ni[:, 2] >= 0
+    assert int(leaf[:r].sum() + leaf[e:].sum()) == info.n_split_leaves
+    inside = ni[r:e, 2][leaf[r:e]]
+    assert set(ti[inside, 0].tolist()) == {int(np.argmax(np.bincount(ti[:, 0])))}   # the bunny mesh only
+    # a node's subtree is [k, k + size): the ancestors of node i are the internal nodes k < i whose subtree
+    # covers it; their boxes contain node i's
+    n = len(nf)
+    size = np.ones(n, np.int64)
+    for k in range(n - 1, -1, -1):
+        if ni[k, 2] < 0:
+            size[k] = 1 + size[ni[k, 0]] + size[ni[k, 1]]
+    assert r + size[r] == e
+    for i in [r] + [k for k in range(n) if leaf[k] and not (r <= k < e)]:
+        anc = [k for k in range(i) if ni[k, 2] < 0 and k + size[k] > i]
+        for k in anc:
+            assert np.all(nf[k, 0:3] <= nf[i, 0:3]) and np.all(nf[k, 3:6] >= nf[i, 3:6]), (i, k)
+    # the small Cornell scene has its leaf-box table instead, no split
+    c = rt.Scene.cornell().info()
+    assert c.split_root == 0 and c.n_split_leaves == 0 and c.n_leaf_boxes > 0
+
+
 def test_oracle_small_image(bunny_raw, fixture):
     meshes = O.cornell_meshes() + [("c5", rt.c5_mesh(bunny_raw), np.array([0.7, 0.7, 0.7], np.float32), np.zeros(3, np.float32))]
     acc, rgba, _ = O.Scene(meshes).render(96, 54, 16, seed=0, threads=min(8, os.cpu_count() or 1))
