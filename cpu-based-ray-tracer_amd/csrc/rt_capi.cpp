@@ -34,7 +34,7 @@ struct rt_ctx {
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr, *d_lboxes = nullptr;
     float4* d_sboxes = nullptr;   // split trace (FlatScene::sboxes): outside leaf boxes
     int32_t* d_stri = nullptr;    // split trace: outside slot -> triangle
-    uint32_t split_root = 0, split_end = 0, n_sboxes = 0;
+    uint32_t split_root = 0, split_end = 0, n_sboxes = 0, n_sleaves = 0;
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
     bool qbvh = false;                             // RT_QBVH=1: the BVH variant walks the compact BVH (A/B: slower)
@@ -521,6 +521,7 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     c->split_root = s->flat.split_root;
     c->split_end = s->flat.split_end;
     c->n_sboxes = (uint32_t)(s->flat.sboxes.size() / 8);
+    c->n_sleaves = (uint32_t)s->flat.stri.size();
     if ((r = upload(c, c->d_qnodes, s->flat.qnodes)) != RT_OK) return r;
     if ((r = upload(c, c->d_tabc, s->flat.tabc)) != RT_OK) return r;
     if ((r = upload(c, c->d_tnrm, s->flat.tnrm)) != RT_OK) return r;
@@ -601,7 +602,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     // the BVH-walking kernels: no leaf-box table, no compact tree
     dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
     dfree(c->d_sboxes); dfree(c->d_stri);   // the split refers to the host tree's node order
-    c->split_root = c->split_end = c->n_sboxes = 0;
+    c->split_root = c->split_end = c->n_sboxes = c->n_sleaves = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
     c->hdr.has_qnodes = 0;
@@ -678,7 +679,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.lboxes = c->d_lboxes; P.n_lboxes = c->brute ? c->hdr.n_lboxes : 0;
     if (c->split && c->split_root != 0 && P.n_lboxes == 0) {
         P.sboxes = c->d_sboxes; P.stri = c->d_stri; P.n_sboxes = c->n_sboxes;
-        P.split_root = c->split_root; P.split_end = c->split_end;
+        P.split_root = c->split_root; P.split_end = c->split_end; P.n_split_leaves = c->n_sleaves;
     }
     P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
     P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;
@@ -746,7 +747,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; materials and the light
         // tables stay in LDS when they are small (C5: 21 quads)
         const uint32_t small = 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris;
-        P.lds_scene_quads = (c->bvh_small_lds && small <= 64u) ? small : 0u;
+        P.lds_small = (c->bvh_small_lds && small <= 64u) ? 1u : 0u;
+        // the split's outside triangles (<= 32 x 3 quads) are staged after them, always
+        P.lds_scene_quads = (P.lds_small ? small : 0u) + 3u * P.n_split_leaves;
         P.ring_pack = (c->ring_pack >= 1 && c->hdr.n_mats <= 8) ? 1u : 0u;
         P.thresh = P.split_root != 0u ? c->sthresh : c->vthresh;
         P.steps = P.split_root != 0u ? c->ssteps : c->vsteps;

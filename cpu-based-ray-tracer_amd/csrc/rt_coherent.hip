@@ -250,7 +250,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     S.n_nodes = P.n_nodes;
     if (BVH) {
         S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = nullptr;
-        if (P.lds_scene_quads != 0u) {
+        uint32_t at = 0;
+        if (P.lds_small != 0u) {
             // the small tables in LDS (mats | lnodes | ltris): the service's material and the light
             // sample then wait on no HBM load
             const uint32_t mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
@@ -260,9 +261,22 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
             for (uint32_t i = threadIdx.x; i < lq; i += blockDim.x) dl[i] = P.lnodes[i];
             for (uint32_t i = threadIdx.x; i < ltq; i += blockDim.x) dlt[i] = P.ltris[i];
-            __syncthreads();
             S.mats = dm; S.lnodes = dl; S.ltris = dlt;
+            at = mq + lq + ltq;
         }
+        if (P.split_root != 0u) {
+            // the split's outside triangles by slot (a, e1, (e2, bits(triangle))): a candidate's
+            // Moller-Trumbore reads LDS instead of a slot -> triangle -> vertices chain of HBM loads
+            float4* ds = lds_scene + at;
+            for (uint32_t i = threadIdx.x; i < 3u * P.n_split_leaves; i += blockDim.x) {
+                const uint32_t k = i / 3u, j = i - 3u * k;
+                const int tri = P.stri[k];
+                float4 v = P.tris[4 * tri + j];
+                if (j == 2u) v.w = __int_as_float(tri);
+                ds[i] = v;
+            }
+        }
+        if (P.lds_scene_quads != 0u) __syncthreads();
     } else {
         // stage the scene into LDS once per workgroup: tris | mats | lnodes | ltris (the BVH nodes stay in
         // HBM -- only a ray with a non-finite reciprocal direction walks them -- and the leaf boxes are read
@@ -990,26 +1004,25 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             // trace or nobody waits for service.
             CKParams& Q = kargs4();
             const uint32_t thresh = Q.thresh, steps = Q.steps;
+            SEC_MARK(2);   // BVH: the split phase (section 2)
             if (Q.split_root != 0u) {
-                // Split trace (rt_scene.cpp): a fresh ray (ti == 0) first tests the <= 64 leaves outside the
+                // Split trace (rt_scene.cpp): a fresh ray (ti == 0) first tests the <= 32 leaves outside the
                 // walked subtree by their own boxes -- one wave-uniform loop of scalar box loads, the
                 // leaf-box variant's trace -- and the subtree's root box; it walks the subtree only when that
                 // box is hit (entered within the bound).  Every ancestor box contains these boxes and the
                 // finite slab test is monotone, so a box's own test decides whether the reference reaches it.
                 // The closest hit is taken by (min t, max triangle) -- triangles are numbered in DFS order --
                 // since the outside leaves are tested before the subtree's.
-                // one ray at a time (A, then B): the box loop and the candidates of one ray live at once
-#pragma nounroll
-                for (uint32_t k = 0; k < 2u; ++k) {
-                    const bool isA = k == 0u;
-                    const bool fresh = in_path && (isA ? tiA : tiB) == 0u && !(!isA && occB);
-                    if (!__any(fresh)) continue;
-                    const V3 d = isA ? dA : dB;
-                    const Ray r{o, d, rcp3(d), d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
-                    const bool fin = finite3(r.rcp) && Q.force_walk == 0u;
-                    // ray A: no bound yet (its first candidates); ray B: no blocker beyond the light point
-                    const float bnd = isA ? __builtin_inff() : slen * 1.00001f + 1e-5f;
-                    uint64_t cm = 0;
+                // both fresh rays at once (the leaf-box variant's NARROW trace): one box loop shares each
+                // box's plane - origin between ray A and ray B, and one candidate loop walks ray A's slots
+                // (low half) then ray B's (high half) -- a wave loops over its busiest lane's A + B
+                // candidates instead of the busiest A plus the busiest B (<= 32 outside leaves, rt_scene.cpp)
+                const bool fA = in_path && tiA == 0u, fB = in_path && tiB == 0u && !occB;
+                if (__any(fA || fB)) {
+                    const V3 rA = rcp3(dA), rB = rcp3(dB);
+                    const bool okA = fA && finite3(rA) && Q.force_walk == 0u, okB = fB && finite3(rB) && Q.force_walk == 0u;
+                    const float bndB = slen * 1.00001f + 1e-5f;   // ray B: no blocker beyond the light point
+                    uint32_t ma = 0, mb = 0;
                     {
                         cbox8* bx = (cbox8*)kargs4().sboxes;
                         const uint32_t nb = kargs4().n_sboxes;
@@ -1018,44 +1031,50 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                             const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
                             const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
                             const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
-                            const uint64_t m = (uint64_t)(uint32_t)f2i(q.s6) | ((uint64_t)(uint32_t)f2i(q.s7) << 32);
-                            cm |= box_hit_pk_within(sx, sy, sz, r.rcp, bnd) ? m : 0ull;
+                            const uint32_t m = (uint32_t)f2i(q.s6);
+                            ma |= box_hit_pk(sx, sy, sz, rA) ? m : 0u;
+                            mb |= box_hit_pk_within(sx, sy, sz, rB, bndB) ? m : 0u;
                         }
                     }
-                    if (!(fresh && fin)) cm = 0;
-                    // the subtree's root box before the candidates (the reciprocals are then dead): for ray A
-                    // without a bound -- the walk's first step tests the root again under the closest outside
-                    // hit; ray B within the light distance.  A walk that leaves the subtree goes on through the
-                    // nodes after it (outside leaves, tested again: the same t and triangle change nothing).
-                    // A ray with a non-finite reciprocal keeps ti = 0 and walks the whole tree in the rounds
-                    // (the std::max/min slab test), like the whole-tree walk.
-                    uint32_t ti = NN;
-                    if (fresh && fin) {
+                    // the subtree's root box (ray A without a bound: the walk's first step tests the root
+                    // again under the closest outside hit; ray B within the light distance)
+                    uint32_t nA = NN, nB = NN;
+                    {
                         const uint32_t root = kargs4().split_root;
                         const float4 n0 = S.nodes[2 * root], n1 = S.nodes[2 * root + 1];
-                        if (slab_hit_finite_within(r, n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, bnd)) ti = root;
+                        const f2 sx = f2{n0.x, n0.w} - f2{o.x, o.x};
+                        const f2 sy = f2{n0.y, n1.x} - f2{o.y, o.y};
+                        const f2 sz = f2{n0.z, n1.y} - f2{o.z, o.z};
+                        if (box_hit_pk(sx, sy, sz, rA)) nA = root;
+                        if (box_hit_pk_within(sx, sy, sz, rB, bndB)) nB = root;
                     }
+                    if (!okA) ma = 0u;
+                    if (!okB) mb = 0u;
+                    uint64_t cm = (uint64_t)ma | ((uint64_t)mb << 32);
                     while (cm != 0) {
-                        const int tri = kargs4().stri[__builtin_ctzll(cm)];
+                        const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
                         cm &= cm - 1;
-                        const float* T = reinterpret_cast<const float*>(S.tris + 4 * tri);   // a, e1, e2 (xyz of 3 float4)
+                        const bool useA = bit < 32u;
+                        // the slot's triangle, staged in LDS after the small tables (a, e1, (e2, bits(triangle)))
+                        const float4* T = lds_scene + (kargs4().lds_small ? 2u * kargs4().n_mats + kargs4().n_lnodes + 4u * kargs4().n_ltris : 0u) + 3u * (bit & 31u);
+                        const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+                        const int tri = f2i(t2.w);
                         double t;
-                        if (moller_trumbore_od(V3{T[0], T[1], T[2]}, V3{T[4], T[5], T[6]}, V3{T[8], T[9], T[10]}, o, d, t)) {
-                            if (isA) {
+                        if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, useA ? dA : dB, t)) {
+                            if (useA) {
                                 if (t < tA || (t == tA && tri > triA)) { tA = t; triA = tri; }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
-                                cm = 0;
-                                ti = NN;
+                                nB = NN;
+                                cm = 0;   // ray B's candidates come last
                             }
                         }
                     }
-                    if (fresh && fin) {
-                        if (isA) tiA = ti;
-                        else tiB = ti;
-                    }
+                    if (okA) tiA = nA;
+                    if (okB) tiB = nB;
                 }
             }
+            SEC_MARK(5);   // BVH: the rounds (walk; the postponed leaves' tests in section 6)
             for (;;) {
                 const bool tracing = in_path && (tiA < NN || tiB < NN);
                 const uint64_t act = __ballot(tracing);

@@ -17,7 +17,9 @@ struct KParams {
     const float4* lboxes; uint32_t n_lboxes;   // small scenes: distinct leaf boxes + triangle masks (rt_layout.h)
     // split trace (larger scenes, the vertex kernel's BVH variant; rt_scene.h FlatScene::sboxes): the rays walk
     // only the subtree [split_root, split_end), the outside leaves are tested by their boxes (split_root = 0: off)
-    const float4* sboxes; const int32_t* stri; uint32_t n_sboxes, split_root, split_end;
+    const float4* sboxes; const int32_t* stri; uint32_t n_sboxes, split_root, split_end, n_split_leaves;
+    uint32_t lds_small;   // the BVH variant: the small tables (mats | lnodes | ltris) are staged in LDS; the split's
+                          // outside triangles (3 float4 per slot: a, e1, (e2, bits(triangle))) follow them
     // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex
     // kernel's BVH variant walks it for waves whose rays all have a finite reciprocal direction
     const uint4* qnodes; const float4* tabc; const float4* tnrm; uint32_t use_qnodes;

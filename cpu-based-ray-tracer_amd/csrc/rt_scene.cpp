@@ -440,8 +440,8 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             }
         }
     }
-    // ---- split trace of a larger scene: the deepest internal node whose subtree leaves at most 64 leaves
-    // outside it (the subtrees with that property form the chain from the root down to it).  The outside
+    // ---- split trace of a larger scene: the deepest internal node whose subtree leaves at most 32 leaves
+    // outside it (the kernel keeps ray A's and ray B's outside candidates in the halves of one mask) (the subtrees with that property form the chain from the root down to it).  The outside
     // leaves are tested by their own boxes, exactly as the small scenes' leaf boxes above (every ancestor
     // box must contain the leaf box), and the subtree is walked from its root, whose box must likewise lie
     // inside every ancestor's: then the root's own slab test decides whether the reference enters it.
@@ -457,7 +457,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             if (fn[i].tri >= 0) continue;
             const uint32_t end = (uint32_t)fn[i].skip;
             const uint32_t outside = n_leaves - (leaf_pre[end] - leaf_pre[i]);
-            if (outside <= 64 && (r == 0 || end - i < (uint32_t)fn[r].skip - r)) r = i;
+            if (outside <= 32 && (r == 0 || end - i < (uint32_t)fn[r].skip - r)) r = i;
         }
         auto inside_ancestors = [&](uint32_t i) {   // every ancestor box of node i contains its box
             const Box& lb = fn[i].box;

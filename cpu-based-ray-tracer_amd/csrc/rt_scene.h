@@ -49,7 +49,7 @@ struct FlatScene {
     std::vector<float> went, wtris;                                       // Whitted world (C1)
     std::vector<float> lboxes;                                            // distinct leaf boxes (small scenes)
     // split trace (larger scenes, the vertex kernel's BVH variant): the subtree [split_root, split_end) of
-    // the DFS pre-order is walked; the <= 64 leaves outside it are tested by their distinct leaf boxes
+    // the DFS pre-order is walked; the <= 32 leaves outside it are tested by their distinct leaf boxes
     // (sboxes: the lboxes layout, the masks over outside slots), slot k = the k-th outside leaf in DFS
     // order = triangle stri[k]; split_root = 0: no split
     std::vector<float> sboxes;

@@ -109,7 +109,7 @@ typedef struct {
     uint32_t split_root;   /* split trace of a larger scene (the vertex kernel's BVH variant): the walked subtree
                               [split_root, split_end) of the DFS pre-order; 0 when the scene has none */
     uint32_t split_end;
-    uint32_t n_split_leaves;   /* leaves outside that subtree, tested by their boxes (<= 64) */
+    uint32_t n_split_leaves;   /* leaves outside that subtree, tested by their boxes (<= 32) */
     uint32_t n_split_boxes;    /* their distinct boxes */
 } rt_scene_info;
 rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);

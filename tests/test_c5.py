@@ -77,13 +77,13 @@ def test_scene_build_matches_reference(scene, fixture):
 
 def test_split_trace_tables(scene):
     """The split trace's host tables (rt_scene.cpp): the walked subtree is the deepest one leaving at most
-    64 leaves outside it -- in C5 the bunny's mesh subtree, with the Cornell box's 32 triangles outside --
+    32 leaves outside it -- in C5 the bunny's mesh subtree, with the Cornell box's 32 triangles outside --
     the outside leaves are exactly the leaves outside [split_root, split_end), every one inside all its
     ancestor boxes, and the subtree's root box inside every ancestor's (leaf-box monotonicity)."""
     info = scene.info()
     nf, ni, tf, ti = scene.export()
     r, e = info.split_root, info.split_end
-    assert r > 0 and e > r and info.n_split_leaves == 32 and 0 < info.n_split_boxes <= 32
+    assert r > 0 and e > r and info.n_split_leaves == 32 and 0 < info.n_split_boxes <= 32   # <= 32 outside leaves
     leaf = ni[:, 2] >= 0
     assert int(leaf[:r].sum() + leaf[e:].sum()) == info.n_split_leaves
     inside = ni[r:e, 2][leaf[r:e]]

@@ -46,7 +46,7 @@ def main():
         # rt_coherent.hip SEC_MARK: [0] top (path ends, fold drain, work / camera records), [1] path end (fold set-up,
         # parked sample), [3] service (shadow verdict, fold level), [4] vertex shading (and the BVH variant's camera
         # ray), [5] box loop (leaf boxes) or BVH rounds, [6] Moller-Trumbore
-        names = ["top: drain + records", "path end", "(unused)", "service", "vertex", "box loop", "moller-trumbore", "(entry)"]
+        names = ["top: drain + records", "path end", "(unused; BVH: split phase)", "service", "vertex", "box loop (BVH: rounds)", "moller-trumbore", "(entry)"]
         tot = float(sum(cyc)) or 1.0
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
         n = c.debug_counters(44)[24:44]
