@@ -382,7 +382,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
-    uint32_t bskip = 0;                       // NARROW: shadow-ray candidates that cannot block (light plane)
+    uint32_t bskip = 0;                       // NARROW / split: shadow-ray candidates that cannot block (light plane)
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
     V3 hloc{0.f, 0.f, 0.f};                   // !BVH: ray A's hit location (from the trace) ...
     bool hflip = false;                       // ... and whether its normal faces away from -dA
@@ -756,7 +756,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     // triangles (near-)coplanar with the sampled light triangle are hit, if at all, within
                     // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
                     // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
-                    if (NARROW && !BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
+                    // (the BVH variant's split phase: the same masks over its outside slots, rt_scene.cpp)
+                    if ((NARROW && !BVH) || BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
                 }
                 // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
                 cont = G.next() < Q.rr && depth < 4096u;
@@ -1049,7 +1050,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         if (box_hit_pk_within(sx, sy, sz, rB, bndB)) nB = root;
                     }
                     if (!okA) ma = 0u;
-                    if (!okB) mb = 0u;
+                    mb = okB ? mb & ~bskip : 0u;   // outside slots near-coplanar with the sampled light triangle
+                    bskip = 0u;
                     uint64_t cm = (uint64_t)ma | ((uint64_t)mb << 32);
                     while (cm != 0) {
                         const uint32_t bit = (uint32_t)__builtin_ctzll(cm);

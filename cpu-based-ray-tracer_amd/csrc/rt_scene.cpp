@@ -661,7 +661,10 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         // 5 * 2^-24 * (|o - a| + t) / (0.1 * 0.2) <= 3e-5 * extent of the true one.  So t > slen - 0.01 and
         // `slen < t + 0.01f` (MC/Renderer.cpp:184) holds: T never occludes.  eta / 0.25 + 6e-5 * extent
         // must stay below 0.008, else no mask is set.
-        if (NT <= 32) {
+        // A split scene (larger scenes, <= 32 leaves outside the walked subtree) gets the same masks over its
+        // outside slots: the kernel's split phase tests those leaves like the narrow build's triangles.
+        const bool split_masks = NT > 32 && !out.stri.empty();
+        if (NT <= 32 || split_masks) {
             double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
             auto vert = [&](uint32_t s, int k, double v[3]) {
                 const float* q = &out.tris[16 * (size_t)s];
@@ -684,7 +687,9 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
                     for (int a = 0; a < 3; ++a) n[a] /= nn;
                     const double d0 = n[0] * lq[0] + n[1] * lq[1] + n[2] * lq[2];
                     uint32_t mask = 0;
-                    for (uint32_t s = 0; s < NT; ++s) {
+                    const uint32_t n_cand = split_masks ? (uint32_t)out.stri.size() : NT;
+                    for (uint32_t k = 0; k < n_cand; ++k) {
+                        const uint32_t s = split_masks ? (uint32_t)out.stri[k] : k;   // mask bit k: triangle s
                         const float* q = &out.tris[16 * (size_t)s];
                         bool near = true;
                         for (int kk = 0; kk < 3 && near; ++kk) {
@@ -698,7 +703,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
                         const double lc = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
                         if (!near || !(lc >= 0.1 * l1 * l2) || !(lc > 0.0)) continue;
                         if (std::fabs((c[0] * n[0] + c[1] * n[1] + c[2] * n[2]) / lc) < 0.999) continue;
-                        mask |= 1u << s;
+                        mask |= 1u << k;
                     }
                     std::memcpy(&lq[3], &mask, 4);
                 }
