@@ -100,9 +100,12 @@ def test_split_trace_tables(scene):
         anc = [k for k in range(i) if ni[k, 2] < 0 and k + size[k] > i]
         for k in anc:
             assert np.all(nf[k, 0:3] <= nf[i, 0:3]) and np.all(nf[k, 3:6] >= nf[i, 3:6]), (i, k)
-    # the small Cornell scene has its leaf-box table instead, no split
+    # the small Cornell scene has its leaf-box table instead, no split; the light-plane skip masks of the
+    # split's outside slots (rt_scene.cpp) mark as many candidates as the Cornell box's own (its light's two
+    # triangles and the ceiling's two, per light triangle)
     c = rt.Scene.cornell().info()
     assert c.split_root == 0 and c.n_split_leaves == 0 and c.n_leaf_boxes > 0
+    assert info.n_light_skip == c.n_light_skip == 8
 
 
 def test_oracle_small_image(bunny_raw, fixture):
