@@ -37,6 +37,7 @@ FLOPS_PER_SAMPLE = (REF_WORK["rays_per_sample"] * (REF_WORK["node_tests_per_ray"
                     + REF_WORK["shading_calls_per_sample"] * 150)
 # MI355X_MICROARCH.md / SURVEY.md 8(d): FP32 vector peak (dense, packed-FMA issue)
 VALU_PEAK_TFLOPS = 157.3
+HBM_PEAK_BYTES_PER_S = 8.0e12   # MI355X_MICROARCH.md: HBM3E
 # VALU issue peak: a wave64 VALU instruction occupies its SIMD-32 for 2 cycles (MI355X_MICROARCH.md),
 # 256 CUs x 4 SIMDs at 2.4 GHz
 VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2
@@ -192,6 +193,52 @@ def cpu_baseline(W, H, seconds):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo):
+    """The metric's second half ("per-pixel RMSE vs CPU ref", BASELINE.json) for the LAST timed frame, after
+    the timed region.  tests/golden/full_c4.npz (and full_c2.npz) hold the reference's frame at the
+    benchmarked configuration's full spp (frames 1..spp, seed 0, RR 0.8; the accumulation of
+    MC/Renderer.cpp:114-133): the SHA-256 of its float4 accumulation and RGBA8 frame, and every 16th row
+    of the accumulation (oracle/gen_golden.py `full`: oracle/_ref/ref_harness, the reference's own MC/ code
+    with the Philox words injected).  Each rank checks the committed rows it owns; rank 0 hashes the
+    gathered RGBA8 frame (and, at N = 1, the whole accumulation).  None for other shapes / FAST mode."""
+    import hashlib
+    fx = None
+    for name in ("full_c4.npz", "full_c2.npz"):
+        p = os.path.join(REPO, "tests", "golden", name)
+        if os.path.exists(p):
+            z = np.load(p)
+            if (int(z["W"]), int(z["H"]), int(z["spp"]), int(z["first_frame"])) == (W, H, spp, 1) and not args.fast:
+                fx = (name, z)
+    if fx is None:
+        return None
+    name, z = fx
+    acc = ctx.accumulation()   # this rank's rows (synchronises; RtError on an EXACT overflow)
+    pos = {int(r): k for k, r in enumerate(z["rows"])}
+    sel = [(li, pos[int(g)]) for li, g in enumerate(ctx.local_to_global_rows()) if int(g) in pos]
+    a = acc[[li for li, _ in sel], :, :3]
+    b = z["accum_rows"][[k for _, k in sel]]
+    ca = np.clip(a / np.float32(spp), 0.0, 1.0).astype(np.float64)   # the average, clamp (MC/Renderer.cpp:130-131)
+    cb = np.clip(b / np.float32(spp), 0.0, 1.0).astype(np.float64)
+    sums = np.array([float(((ca - cb) ** 2).sum()), float(np.all(a.view(np.uint32) == b.view(np.uint32), axis=-1).sum()),
+                     float(a.shape[0] * a.shape[1]), float(np.abs(ca - cb).max(initial=0.0))], np.float64)
+    if world > 1:
+        t = torch.tensor(sums[:3], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
+        dist.all_reduce(t)
+        m = torch.tensor(sums[3:], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        sums = np.concatenate([t.cpu().numpy(), m.cpu().numpy()])
+    out = {"fixture": f"tests/golden/{name}", "rows_checked": int(sums[2] // W), "rows_stride": int(z["rows"][1] - z["rows"][0]),
+           "rmse_vs_ref": float(np.sqrt(sums[0] / max(1.0, 3.0 * sums[2]))), "max_abs_diff": float(sums[3]),
+           "bitwise_frac": float(sums[1] / max(1.0, sums[2]))}
+    if gat.rank == 0:
+        img = gat.image.cpu().numpy().view(np.uint32).reshape(H, W)
+        out["sha_rgba_match"] = hashlib.sha256(np.ascontiguousarray(img).tobytes()).hexdigest() == str(z["sha_rgba"])
+        if world == 1:
+            out["sha_accum_match"] = hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest() == str(z["sha_accum"])
+        out["sha_match"] = bool(out["sha_rgba_match"] and out.get("sha_accum_match", True) and out["bitwise_frac"] == 1.0)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,6 +332,8 @@ def main():
     value = total_samples / elapsed / 1e6
     if args.dump_image and rank == 0:
         np.save(args.dump_image, gat.image.cpu().numpy().view(np.uint32).reshape(H, W))
+    # the metric's second half: the last timed frame against the reference (outside the timed region)
+    parity = frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo)
 
     # Roofline of the path's kernels on this rank.  SURVEY.md 8(d): there is no dense contraction and the
     # Cornell scene lives on chip, so the binding roof for C2/C4 is the vector ALU; the sample is priced by
@@ -319,6 +368,9 @@ def main():
         # a rocprofv3 counter pass of this build and shape (profiles/): HBM bytes per launch and the
         # kernels' VALU issue fraction / lane utilization
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        # the path kernel's measured L2 -> fabric bytes per launch over its live launch time, against HBM's 8 TB/s
+        if roof["traffic"] and main_s > 0:
+            roof["hbm_frac_measured"] = round(roof["traffic"] / main_s / HBM_PEAK_BYTES_PER_S, 4)
         roof["counters"] = {"file": pmc["_file"], "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
                             "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                             "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample"),
@@ -357,6 +409,7 @@ def main():
                        "seed": 0, "band_rows": args.band, "accumulation": "fast" if args.fast else "exact",
                        "parallelism": f"row-bands x{world}", "dist_backend": args.dist_backend if world > 1 else None},
             "roofline": roof,
+            "parity": parity,
             "fast_mode": fast,
             "rank_elapsed_s": [round(x, 6) for x in per_rank],
             "cpu_baseline": cpu,

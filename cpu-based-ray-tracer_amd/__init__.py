@@ -16,6 +16,9 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 
+# include/rt_capi.h RT_API_VERSION: the struct layouts (rt_stats, rt_scene_info, ...) this binding declares
+API_VERSION = 2
+
 RT_OK = 0
 RT_ERR_OVERFLOW = -6
 RENDER_EXACT = 1
@@ -166,6 +169,10 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    v = L.rt_api_version()
+    if v != API_VERSION:
+        # a library built from another header revision would read / write structs of another size
+        raise RtError(f"{LIB_PATH}: C-ABI version {v}, this binding needs {API_VERSION} (rebuild with `make -C {PKG_DIR}`)")
     _lib = L
     return L
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "rt_kernels.h"
+#include "rt_knobs.h"
 #include "rt_scene.h"
 
 struct rt_scene {
@@ -93,7 +94,7 @@ struct rt_ctx {
     // (tuned on MI355X at N=1 and on an 8-way row band; RT_CHUNKS forces a count)
     uint32_t force_chunks = 0, items_per_lane = 64, min_px_per_lane = 32, min_chunk_frames = 8;
     uint64_t lbuf_budget = 96ull << 30;   // bytes of parked samples (+ camera records) per launch; C4 needs 59 GB of 288
-    bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(32 GB, 3/4 of free memory) per render
+    bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(96 GB, 3/4 of free memory) per render
     float* d_lbuf = nullptr;
     size_t lbuf_floats = 0;
     // the vertex kernel's camera pre-pass: surface-hit records, per-segment counts, the non-empty segments
@@ -412,29 +413,29 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     rt_ctx* c = new (std::nothrow) rt_ctx;
     if (!c) return RT_ERR_OOM;
     c->device = cfg ? cfg->device : 0;
-    if (const char* e = std::getenv("RT_THRESH")) c->thresh = c->vthresh = c->sthresh = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_STEPS")) c->steps = c->vsteps = c->ssteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
-    if (const char* e = std::getenv("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = std::getenv("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
-    if (const char* e = std::getenv("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = std::getenv("RT_MIN_CHUNK_FRAMES")) c->min_chunk_frames = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
-    if (const char* e = std::getenv("RT_LBUF_BUDGET_MB")) {
+    if (const char* e = rt_knob("RT_THRESH")) c->thresh = c->vthresh = c->sthresh = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_STEPS")) c->steps = c->vsteps = c->ssteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_MIN_PX_PER_LANE")) c->min_px_per_lane = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_MIN_CHUNK_FRAMES")) c->min_chunk_frames = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_LBUF_BUDGET_MB")) {
         c->lbuf_budget = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) << 20;
         c->lbuf_budget_env = true;
     }
-    if (const char* e = std::getenv("RT_STACK_DEPTH")) c->stack_depth_force = std::min<uint32_t>(kStackDepthMax, (uint32_t)std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_STACK_DEPTH")) c->stack_depth_force = std::min<uint32_t>(kStackDepthMax, (uint32_t)std::strtoul(e, nullptr, 10));
     hipError_t e = hipSetDevice(c->device);
     if (e != hipSuccess) { rt_status s = hip_fail(c, e, "hipSetDevice"); std::fprintf(stderr, "rt_create: %s\n", c->err.c_str()); delete c; return s; }
     if (cfg && cfg->stream) {
@@ -656,6 +657,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (exact) {
         // the fold stack / ring, sized from rr (reallocated when a render needs more levels)
         const uint32_t want = c->stack_depth_force ? std::max<uint32_t>(1, c->stack_depth_force) : stack_levels_for(p->rr);
+        // (the vertex kernel indexes the ring in 32 bits: lane * depth + position, rt_coherent.hip RING_AT)
+        if ((uint64_t)want * c->total_threads >= (1ull << 32)) { c->err = "fold ring index exceeds 32 bits"; return RT_ERR_INVALID; }
         if (!c->d_stack_ld || want > c->stack_depth || (c->stack_depth_force && want != c->stack_depth)) {
             HIPC(c, hipStreamSynchronize(c->stream));
             dfree(c->d_stack_ld); dfree(c->d_stack_mat);
@@ -734,8 +737,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
     // any other path scene: its BVH variant, the scene in HBM (RT_VERTEX_BVH=0: the megakernel)
     const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
-    // (the camera pre-pass's records carry a triangle index in 19 bits, rt_kernels.h crec)
-    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 19);
+    // (the camera pre-pass's records carry a triangle index in 19 bits, rt_kernels.h crec: only the leaf-box
+    // variant runs the pre-pass, and its scenes have <= 64 triangles; the BVH variant carries full indices)
+    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31);
     const bool coh = coh_box || coh_bvh;
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
@@ -809,15 +813,27 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             uint32_t passes = 1;
             if (!c->lbuf_budget_env) {
                 // parked-sample budget from the device's free memory (the current buffer counts as free):
-                // at most 32 GB, at most 3/4 of what is free
+                // at most 96 GB, at most 3/4 of what is free
                 size_t fr = 0, tot = 0;
                 HIPC(c, hipMemGetInfo(&fr, &tot));
                 c->lbuf_budget = std::max<uint64_t>(64ull << 20, std::min<uint64_t>(96ull << 30, (fr + c->lbuf_floats * sizeof(float) + c->crec_quads * sizeof(float4)) / 4 * 3));
             }
             if (want > 1 || park_all) {
-                // parked samples (12 B); the vertex kernel's camera records too (16 B)
-                const uint64_t bytes = px_local * (uint64_t)p->n_frames * (coh_box ? 28ull : 12ull);
-                passes = (uint32_t)std::min<uint64_t>(p->n_frames, (bytes + c->lbuf_budget - 1) / c->lbuf_budget);
+                // the bytes one pass of nf frames allocates: parked samples (12 B, frames in 4-frame blocks) and,
+                // for the leaf-box variant, the camera records (16 B per 8x8-padded tile pixel and frame, the
+                // frames rounded up to whole pre-pass segments of min(64, the next power of two) frames)
+                auto pass_bytes = [&](uint64_t nf) {
+                    uint64_t b = 12ull * px_local * ((nf + 3) & ~3ull);
+                    if (coh_box) {
+                        uint64_t sf = 1;
+                        while (sf < nf && sf < 64) sf <<= 1;
+                        b += 16ull * items_px * ((nf + sf - 1) / sf * sf);
+                    }
+                    return b;
+                };
+                const uint64_t nfr = p->n_frames;
+                passes = (uint32_t)std::min<uint64_t>(nfr, std::max<uint64_t>(1, pass_bytes(nfr) / c->lbuf_budget));
+                while (passes < nfr && pass_bytes((nfr + passes - 1) / passes) > c->lbuf_budget) ++passes;
             }
             uint32_t done = 0;
             for (uint32_t pass = 0; pass < passes; ++pass) {

@@ -18,6 +18,7 @@
 #include "rt_device.h"
 #include "rt_glibc_math.h"
 #include "rt_kernels.h"
+#include "rt_knobs.h"
 
 using namespace rtd;
 
@@ -301,13 +302,13 @@ hipError_t rt_launch_denoise(const DenoiseParams& D, hipStream_t stream)
     if (tiles == 0) return hipSuccess;
     if (D.jbf_half > 0) {
         DenoiseParams Dl = D;
-        Dl.ieee_div = getenv("RT_JBF_IEEE") ? 1 : 0;   // diagnostic: every division by the IEEE sequence (tests)
-        if (D.jbf_half <= JB_MAX_HALF && !getenv("RT_JBF_GLOBAL")) {
+        Dl.ieee_div = rt_knob("RT_JBF_IEEE") ? 1 : 0;   // diagnostic: every division by the IEEE sequence (tests)
+        if (D.jbf_half <= JB_MAX_HALF && !rt_knob("RT_JBF_GLOBAL")) {
             // 8 x 64 blocks (8 waves) for wide windows: the ring's halo rows are shared by twice the pixels
             // and 6 waves per SIMD fit instead of 4 (DN65 13.8 -> 12.6 ms); 8 x 32 below a half width of 24
             // (DN33 3.41 ms against 3.66); the 8 x 64 ring must fit 64 KiB of LDS: half widths up to 64.
             // RT_JBF_TALL=32/64 forces one (A/B, tests)
-            const int want = getenv("RT_JBF_TALL") ? atoi(getenv("RT_JBF_TALL")) : (D.jbf_half >= 24 ? 64 : 32);
+            const int want = rt_knob("RT_JBF_TALL") ? atoi(rt_knob("RT_JBF_TALL")) : (D.jbf_half >= 24 ? 64 : 32);
             const int jbh = (want == 64 && D.jbf_half <= 64) ? 64 : 32;
             const uint32_t blocks = (uint32_t)(((D.W + JBW - 1) / JBW) * ((D.H + jbh - 1) / jbh));
             const size_t lds = (size_t)9 * JSLOTS * jbf_pitch(jbh, D.jbf_half) * sizeof(float);

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "rt_capi.h"
+#include "rt_knobs.h"
 
 struct rt_group {
     std::vector<int> dev;
@@ -124,7 +125,7 @@ rt_status rt_group_create(rt_group** out, const int32_t* devices, uint32_t n)
     std::vector<int> sorted(g->dev);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    const char* mode = std::getenv("RT_GROUP_GATHER");
+    const char* mode = rt_knob("RT_GROUP_GATHER");
     g->rccl = distinct && !(mode && std::strcmp(mode, "copy") == 0);
     if (g->rccl) {
         g->comm.assign(n, nullptr);

@@ -171,6 +171,8 @@ Renderer::Renderer() : Renderer(Settings{}, true) {}
 
 Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
 {
+    if (rt_api_version() != RT_API_VERSION)   // this header's structs against the loaded library's
+        throw rt::Error("librt_hip.so C-ABI version " + std::to_string(rt_api_version()) + ", include/rt_capi.h " + std::to_string(RT_API_VERSION));
     if (settings.devices.size() > 1) {
         check(rt_group_create(&group, settings.devices.data(), (uint32_t)settings.devices.size()), "rt_group_create");
     } else {
@@ -194,6 +196,7 @@ Renderer::~Renderer()
 {
     rt_group_destroy(group);
     rt_destroy(ctx);
+    rt_scene_destroy(scene_);
 }
 
 void Renderer::GenerateBVH()
@@ -210,8 +213,9 @@ void Renderer::GenerateBVH()
     }
     rt_status st = rt_scene_build(sc);
     if (st == RT_OK) st = group ? rt_group_upload_scene(group, sc) : rt_upload_scene(ctx, sc);
-    rt_scene_destroy(sc);
-    check(st, "GenerateBVH");
+    if (st != RT_OK) { rt_scene_destroy(sc); check(st, "GenerateBVH"); }
+    rt_scene_destroy(scene_);
+    scene_ = sc;   // kept for Scene()
     bvh_dirty = false;
 }
 

@@ -514,7 +514,8 @@ __global__ void __launch_bounds__(256) whitted_world_kernel(KParams P)
 
 hipError_t rt_launch_whitted_world(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out)
 {
-    const uint32_t tiles = ((P.W + 7) / 8) * ((P.n_local_rows + 7) / 8);
+    // one block per 16x16 tile, whitted_world_kernel's blockIdx -> tile mapping
+    const uint32_t tiles = ((P.W + 15) / 16) * ((P.n_local_rows + 15) / 16);
     if (grid_out) *grid_out = tiles;
     if (tiles == 0) return hipSuccess;
     if (P.max_bounce_depth + 2 > kWorldFrames) return hipErrorInvalidValue;   // the explicit stack bounds the recursion

@@ -92,6 +92,9 @@ public:
     void Add(rt::Entity* entity_pointer) { entities.push_back(entity_pointer); }
     void GenerateBVH();
     float LastKernelMilliseconds() const;
+    // the flattened scene of the last GenerateBVH (host side: rt_scene_get_info / rt_scene_export), e.g. to
+    // check a scene built through Add against the reference's BVH
+    const rt_scene* Scene() const { return scene_; }
 
     float RR_survival_probability = 0.8f;        // MC/Renderer.h:199
     std::vector<rt::Entity*> entities;
@@ -106,6 +109,7 @@ private:
     rt_ctx* ctx = nullptr;
     rt_group* group = nullptr;   // Settings::devices with more than one entry
     std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
+    rt_scene* scene_ = nullptr;
     bool bvh_dirty = true;
 };
 

@@ -15,6 +15,7 @@
 
 #include "Walnut/Image.h"
 #include "Camera.h"
+#include "Whitted.h"   // Whitted::TriangleMesh / WhittedMaterial / Entity, as MC/Renderer.h brings them
 #include "../Renderer.h"
 
 class Renderer {
@@ -45,8 +46,9 @@ public:
     void Reaccumulate() { core_.Reaccumulate(); }
     uint32_t GetSPP() { return core_.GetSPP(); }
     Settings& GetSettings() { return core_.GetSettings(); }
-    [[nodiscard]] const std::vector<rt::Entity*>& GetEntities() const { return core_.GetEntities(); }
-    void Add(rt::Entity* entity_pointer) { core_.Add(entity_pointer); }
+    // the scene-extension API, MC/Renderer.h:72-86: Add(new Whitted::TriangleMesh(path, material)) then GenerateBVH()
+    [[nodiscard]] const std::vector<Whitted::Entity*>& GetEntities() const { return core_.GetEntities(); }
+    void Add(Whitted::Entity* entity_pointer) { core_.Add(entity_pointer); }
     void GenerateBVH() { core_.GenerateBVH(); }
 
     float RR_survival_probability = 0.8f;   // MC/Renderer.h:199 (read at every Render)

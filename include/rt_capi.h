@@ -34,7 +34,9 @@
 extern "C" {
 #endif
 
-#define RT_API_VERSION 1
+/* 2 (round 4): rt_stats grew last_prepass_ms / last_main_ms, rt_scene_info the light-skip and split fields,
+ * rt_read_accumulation was added; a host built against another version must not pass its structs */
+#define RT_API_VERSION 2
 
 typedef int32_t rt_status;
 #define RT_OK 0
@@ -249,7 +251,7 @@ rt_status rt_debug_counters(rt_ctx* ctx, uint64_t* out, uint32_t n);
  * into the full frame there.  The gather is RCCL (ncclGather over one communicator per member,
  * ncclCommInitAll, issued as one group) when the member devices are distinct, device-to-device copies
  * when a device repeats (RCCL takes one rank per GPU; e.g. n members on one GPU in tests) or when
- * RT_GROUP_GATHER=copy.  Every pixel is the same as in a one-device render: the random stream is keyed by
+ * RT_GROUP_GATHER=copy (a debug knob, read only with RT_DEBUG_KNOBS=1).  Every pixel is the same as in a one-device render: the random stream is keyed by
  * the global pixel. */
 typedef struct rt_group rt_group;
 rt_status rt_group_create(rt_group** out, const int32_t* devices, uint32_t n);

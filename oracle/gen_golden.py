@@ -12,6 +12,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py c1         # only the C1 (Whitted two-sphere world) fixtures
     python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
+    python oracle/gen_golden.py full       # C2 and C4 at their full spp (full_c2 / full_c4: one of them)
 """
 import os
 import subprocess
@@ -238,6 +239,32 @@ def gen_images():
         out[f"rgba_{key}"] = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
         out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
     np.savez_compressed(os.path.join(GOLDEN, "images_cornell.npz"), **out)
+
+
+FULL_CONFIGS = [("c2", 784, 784, 256), ("c4", 1920, 1080, 1024)]
+FULL_ROW_STRIDE = 16
+
+
+def gen_full(which=None):
+    """The benchmarked Cornell configurations at their FULL spp: C2 784x784x256 and
+    C4 1920x1080x1024, seed 0, RR 0.8, frames 1..spp (MC/Renderer.cpp:114-133 accumulation over all frames).
+    Stores the SHA-256 of the float4 accumulation and of the RGBA8 frame, and every 16th row of the
+    accumulation's rgb (rows 0, 16, 32, ...), from which bench.py and the GPU tests compute RMSE / bitwise
+    fractions.  C4 takes about 5 minutes on 8 cores."""
+    import hashlib
+    for (name, W, H, spp) in FULL_CONFIGS:
+        if which not in (None, name):
+            continue
+        run("image", CORNELL_DIR, "", W, H, spp, 0, 0.8, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        rows = np.arange(0, H, FULL_ROW_STRIDE)
+        np.savez_compressed(os.path.join(GOLDEN, f"full_{name}.npz"), W=np.int64(W), H=np.int64(H), spp=np.int64(spp),
+                            seed=np.int64(0), rr=np.float32(0.8), first_frame=np.int64(1),
+                            sha_accum=np.array(hashlib.sha256(acc.tobytes()).hexdigest()),
+                            sha_rgba=np.array(hashlib.sha256(rgba.tobytes()).hexdigest()),
+                            rows=rows.astype(np.int64), accum_rows=np.ascontiguousarray(acc[rows, :, :3]),
+                            rgba_rows=np.ascontiguousarray(rgba[rows]), stats=np.fromfile(tmp("stats"), "<u8"))
 
 
 def gen_stat():
@@ -568,6 +595,8 @@ def main():
             gen_dn()
         if only in ("all", "c5"):
             gen_c5(np.random.default_rng(20261016))
+        if only in ("all", "full", "full_c2", "full_c4"):
+            gen_full(None if only in ("all", "full") else only[5:])
     print("golden fixtures written to", GOLDEN)
 
 

@@ -1,5 +1,5 @@
 """bench.py's N > 1 path, run as the driver runs it (torch.distributed.run, one process per rank) with
-two ranks on the box's one GPU: each rank renders its row bands with the HIP kernels, the bands are
+two and eight ranks on the box's one GPU: each rank renders its row bands with the HIP kernels, the bands are
 all-gathered (gloo on host-staged bands: RCCL needs one GPU per rank) and reassembled on rank 0; the
 time is the MAX over ranks.  The JSON line must report the whole job (n_gpus 2, both ranks' times, value
 from the slowest) and rank 0's reassembled frame must equal the one-rank frame bit for bit (the RNG is
@@ -27,21 +27,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_bench_world2_gloo_matches_one_rank(tmp_path):
+@pytest.mark.parametrize("world,W,H", [(2, W, H), (8, 64, 1080)])
+def test_bench_gloo_matches_one_rank(tmp_path, world, W, H):
+    """world 2, and world 8 -- the size the driver's scaling run launches -- on C4's 1080 rows: 135 bands of 8
+    rows over 8 ranks, so 7 ranks own 17 bands and one owns 16 (the gather pads the short rank)"""
     img = tmp_path / "frame.npy"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-           "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", str(world), "--dist-backend", "gloo",
            "--steps", "2", "--warmup", "1", "--width", str(W), "--height", str(H), "--spp", str(SPP), "--no-cpu-baseline",
            "--no-fast-probe", "--dump-image", str(img)]
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     line = json.loads(lines[0])
-    assert line["n_gpus"] == 2 and line["config"]["dist_backend"] == "gloo"
+    assert line["n_gpus"] == world and line["config"]["dist_backend"] == "gloo"
     ranks = line["rank_elapsed_s"]
-    assert len(ranks) == 2
+    assert len(ranks) == world
     # value is the whole job over the slowest rank's time
     assert abs(line["value"] - W * H * SPP * 2 / max(ranks) / 1e6) <= 1e-2 * line["value"]
     assert line["roofline"]["kernel_ms"] > 0

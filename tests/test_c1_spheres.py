@@ -93,6 +93,7 @@ def test_images_bitwise(ctx, fixture, W, H, spp):
     assert hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest() == str(fixture[f"sha_accum_{key}"])
     st = ctx.stats()
     assert st.rays == int(fixture[f"stats_{key}"][0]) * spp   # the same rays per frame as the reference
+    assert st.grid == ((W + 15) // 16) * ((H + 15) // 16)      # one block per 16x16 tile, no idle blocks
 
 
 @pytest.mark.gpu

@@ -33,9 +33,11 @@ def single(W, H, spp, seed=3, first_frame=1, ctx=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,band,W,H", [([0, 0], 8, 96, 72), ([0, 0, 0], 8, 83, 61), ([0, 0, 0, 0], 4, 64, 50)])
+@pytest.mark.parametrize("devices,band,W,H", [([0, 0], 8, 96, 72), ([0, 0, 0], 8, 83, 61), ([0, 0, 0, 0], 4, 64, 50),
+                                             ([0] * 8, 8, 40, 1080)])
 def test_group_copy_gather_equals_one_device(devices, band, W, H):
-    """members on one GPU (copy gather), ragged band counts: RGBA8 and accumulation bitwise equal"""
+    """members on one GPU (copy gather), ragged band counts: RGBA8 and accumulation bitwise equal; eight members
+    over C4's 1080 rows (135 bands: seven members own 17, one 16)"""
     c, rgba1, acc1 = single(W, H, 8)
     c.close()
     g = rt.Group(devices)

@@ -69,3 +69,56 @@ def test_reference_layer_runs_on_the_dropin(tmp_path):
     assert np.array_equal(f3, render(moved, 2, seed=4, rr=0.5))
     assert not np.array_equal(f3, render(cam, 2, seed=4, rr=0.5))
     assert "1 spp" in r.stdout.splitlines()   # the layer's own spp counter (GetSPP)
+
+
+# ------------------------------------------------------------------ the scene-extension spelling (C5)
+def test_scene_extension_compiles_against_the_dropin(tmp_path):
+    """tests/walnut_stub/c5_scene.cpp extends the scene the reference's way -- Whitted::WhittedMaterial,
+    `renderer.Add(new Whitted::TriangleMesh(path, white))`, `GenerateBVH()` (MC/Renderer.h:78-86,
+    MC/TriangleMesh.h:148-186, MC/WhittedMaterial.h:24-42) -- and compiles against include/rt/walnut/*.h."""
+    out = WB.build_c5(str(tmp_path / "walnut_c5_scene"))
+    assert os.path.exists(out)
+
+
+@pytest.mark.gpu
+def test_scene_extension_builds_c5(tmp_path):
+    """C5 built through the drop-in's Whitted:: types: the flattened tree is the reference's
+    (the SHA-256 digest of tests/golden/c5_scene.npz, from the reference's own TriangleMesh + BVH code) and 16
+    frames through Renderer::Render give the reference's 96x54x16 accumulation bit for bit."""
+    import importlib.util
+    import _oracle as O
+    if not os.path.exists(WB.C5_BIN):
+        pytest.skip("tests/_bin/walnut_c5_scene not built (build() builds it)")
+    fx = np.load(os.path.join(O.GOLDEN, "c5_scene.npz"))
+    bunny = np.load(os.path.join(O.GOLDEN, "bvh_scene.npz"))["raw_bunny"]
+    obj = str(tmp_path / "c5_bunny.obj")
+    rt.write_obj(obj, rt.c5_mesh(bunny))
+    prefix = str(tmp_path / "c5")
+    r = subprocess.run([WB.C5_BIN, obj, prefix], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "entities 7" in r.stdout and "16 spp" in r.stdout, r.stdout
+    raw = np.fromfile(prefix + "_scene.bin", np.uint8)
+    nn, nt = raw[:8].view(np.uint32)
+    off = 8
+    def take(dt, n):
+        nonlocal off
+        v = raw[off:off + 4 * n].view(dt)
+        off += 4 * n
+        return v
+    nf = take(np.float32, 7 * nn).reshape(nn, 7); ni = take(np.int32, 5 * nn).reshape(nn, 5)
+    tf = take(np.float32, 13 * nt).reshape(nt, 13); ti = take(np.int32, 2 * nt).reshape(nt, 2)
+    spec = importlib.util.spec_from_file_location("gg", os.path.join(O.ORACLE_DIR, "gen_golden.py"))
+    gg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gg)
+    nodes = np.zeros(nn, gg.NODE_DT)
+    nodes["mn"], nodes["mx"], nodes["area"] = nf[:, 0:3], nf[:, 3:6], nf[:, 6]
+    for k, col in (("left", 0), ("right", 1), ("tri", 2), ("mesh", 3), ("top", 4)):
+        nodes[k] = ni[:, col]
+    tris = np.zeros(nt, gg.TRI_DT)
+    for k, sl in (("a", slice(0, 3)), ("b", slice(3, 6)), ("c", slice(6, 9)), ("n", slice(9, 12))):
+        tris[k] = tf[:, sl]
+    tris["mesh"] = ti[:, 0]
+    assert nn == int(fx["n_nodes"]) and nt == int(fx["n_tris"])
+    assert gg.scene_digest(nodes, tris) == str(fx["digest"])
+    acc = np.fromfile(prefix + "_accum.bin", np.float32).reshape(54, 96, 4)
+    assert np.array_equal(acc.view(np.uint32), fx["accum_96x54_spp16_s0"].view(np.uint32))

@@ -15,6 +15,8 @@ used is in each line.
 import argparse
 import json
 import os
+
+os.environ.setdefault("RT_DEBUG_KNOBS", "1")   # the library reads its A/B knobs only behind this gate (csrc/rt_knobs.h)
 import sys
 
 import numpy as np
@@ -29,9 +31,22 @@ VALU_PEAK_TFLOPS = 157.3
 WORK = {"C1": None, "C2": (5.700, 27.84, 4.06), "C3": None, "C4": (3.645, 24.61, 3.57), "C5": (3.660, 31.30, 3.85)}
 
 
+# Whitted renders, priced the same way:
+#  * C3 (BVH bunny + teapot): SURVEY.md 8(d)'s 1.446 rays/sample, 38.26 box tests and 2.57 triangle tests per ray
+#    = 1196 flops/sample (SURVEY's "~1.2 kflop"; the Phong shading is not priced, as there);
+#  * C1 (two spheres): 2.3078 rays/sample (the reference's own count, tests/golden/c1_spheres.npz stats), each
+#    ray tested brute force against 2 spheres (~25 flops: QuadraticFormula, WH/Sphere.h:26-59) and the 2
+#    chessboard triangles (54), plus 150 for the Phong / Fresnel shading = 308 flops per ray.
+WHITTED_FLOPS = {"C3": 1.446 * (38.26 * 18 + 2.57 * 54), "C1": 2.3078 * (2 * 25 + 2 * 54 + 150)}
+# the joint bilateral filter's tap (DN/Denoiser.h:188-205), counted op by op: position / color / normal /
+# coplanarity distances (differences, dots, the four 2 sigma^2 products and divisions, normalize, squares;
+# acosf ~20 and expf ~15 operations), the weight and the weighted color sum: ~97 fp32 operations
+JBF_FLOPS_PER_TAP = 97.0
+
+
 def flops_per_sample(c):
-    if WORK[c] is None:   # C1 / C3: Whitted renders (one primary ray per pixel, no path sampling)
-        return None
+    if c in WHITTED_FLOPS:
+        return WHITTED_FLOPS[c]
     r, n, t = WORK[c]
     return r * (n * 18 + t * 54) + 0.4036 * r * 150
 
@@ -71,10 +86,15 @@ def main():
                 st = ctx.stats()
                 if f > 1:
                     gms.append(st.last_kernel_ms); dms.append(st.last_denoise_ms)
+            taps = W * H * (2 * half + 1) ** 2
+            dn_s = float(np.median(dms)) / 1e3
+            roof = {"bound": "valu", "flops_per_tap": JBF_FLOPS_PER_TAP, "achieved_tflops": round(taps * JBF_FLOPS_PER_TAP / dn_s / 1e12, 3),
+                    "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(taps * JBF_FLOPS_PER_TAP / dn_s / 1e12 / VALU_PEAK_TFLOPS, 4),
+                    "time": "joint bilateral + temporal kernels (the temporal filter's taps are not priced)"}
             print(json.dumps({"config": c, "width": W, "height": H, "jbf_half_size": half, "temporal_half_size": 3,
                               "gbuffer_ms": round(float(np.median(gms)), 3), "denoise_ms": round(float(np.median(dms)), 3),
                               "frame_ms": round(float(np.median(gms)) + float(np.median(dms)), 3),
-                              "jbf_taps_per_s": round(W * H * (2 * half + 1) ** 2 / (float(np.median(dms)) / 1e3) / 1e9, 2)}), flush=True)
+                              "jbf_taps_per_s": round(taps / dn_s / 1e9, 2), "roofline": roof}), flush=True)
             ctx.close()
             continue
         ctx = rt.Context(0)

@@ -4,6 +4,8 @@ one context per budget, in one process.   python tools/c5_passes.py --spp 4096 -
 import argparse
 import json
 import os
+
+os.environ.setdefault("RT_DEBUG_KNOBS", "1")   # the library reads its A/B knobs only behind this gate (csrc/rt_knobs.h)
 import sys
 import time
 

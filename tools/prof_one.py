@@ -9,6 +9,8 @@ import json
 import importlib.util
 import os
 
+os.environ.setdefault("RT_DEBUG_KNOBS", "1")   # the library reads its A/B knobs only behind this gate (csrc/rt_knobs.h)
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
 

@@ -8,6 +8,8 @@ row band of an N-rank frame (--rank/--nranks) to see multi-GPU per-rank behaviou
 import argparse
 import json
 import os
+
+os.environ.setdefault("RT_DEBUG_KNOBS", "1")   # the library reads its A/B knobs only behind this gate (csrc/rt_knobs.h)
 import sys
 
 import numpy as np

@@ -7,6 +7,8 @@ process, interleaved rounds (cdna guide rule 24).  Prints one JSON line per sett
 import argparse
 import json
 import os
+
+os.environ.setdefault("RT_DEBUG_KNOBS", "1")   # the library reads its A/B knobs only behind this gate (csrc/rt_knobs.h)
 import sys
 
 import numpy as np
