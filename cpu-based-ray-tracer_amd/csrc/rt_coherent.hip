@@ -50,9 +50,12 @@ enum : uint32_t {
     VS_DPOS = 12,                        // EXACT drain: ring position of the next level to fold
     VS_DT0 = 13, VS_DT1 = 14,            // EXACT drain: the sample's local pixel and frame index
     VS_THR = 8, VS_LSUM = 11,            // FAST: throughput, radiance
-    VS_WORDS_EXACT = 15, VS_WORDS_FAST = 14,
-    VS_RNG = 15,                         // unlit scenes only: the Philox block of the current 4 draws
-    VS_WORDS_UNLIT = 19
+    VS_PEND = 15,                        // EXACT, leaf-box variant: a finished path's fold waiting behind the draining
+                                         // one -- ring position of its top level | its levels << 12 (PEND_NONE: none)
+    VS_PLOC = 16,                        //   ... and its sample's local pixel (its L and frame index: the ring slot above its top)
+    VS_WORDS_EXACT = 17, VS_WORDS_FAST = 14,
+    VS_RNG = 17,                         // unlit scenes only: the Philox block of the current 4 draws
+    VS_WORDS_UNLIT = 21
 };
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
@@ -227,12 +230,20 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_DRAIN_BATCH
 #define RT_DRAIN_BATCH 2
 #endif
+// pending fold (leaf-box variant, EXACT): a path that ends while the lane's previous fold still drains parks
+// its own fold behind it (one ring slot holds its L and frame index) instead of completing the draining one
+// at once -- that completion ran a whole fold loop for the one or two lanes that needed it in 83 % of the
+// wave iterations (profiles/r03/c5_final/sections_c4_256spp.txt: fin_iters_with_drain)
+#ifndef RT_PEND_FOLD
+#define RT_PEND_FOLD 1
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
 // fold ring layout: lane-major ([thread][position]): a lane's consecutive levels share cache lines, so a
 // drain read follows its push in L2
-#define RING_AT(p) ((size_t)gtid * Q.stack_depth + (p))
+// (a 32-bit index: lanes x depth < 2^32, checked on the host; one register for the lane's base, no 64-bit product)
+#define RING_AT(p) ((uint32_t)(gtid * Q.stack_depth + (p)))
 
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
@@ -342,11 +353,42 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         pos = pos >= n ? pos - n : pos + R - n;
         return n;
     };
-    // the top of an iteration: DRAIN_STEP levels of the draining fold
+    // the pending fold (PEND): a finished path's fold waiting behind the draining one (lane flag hasPend; its
+    // ring position | levels << 12 in VS_PEND, its local pixel in VS_PLOC, and (L, frame index) in the ring slot
+    // above its top level)
+    constexpr bool PEND = EXACT && !BVH && RT_PEND_FOLD != 0;
+    bool hasPend = false;
+    auto pend_meta_at = [&](uint32_t pd) -> size_t {
+        CKParams& Q = kargs4();
+        uint32_t mp = (pd & 0xFFFu) + 1u;
+        if (mp >= Q.stack_depth) mp -= Q.stack_depth;
+        return RING_AT(mp);
+    };
+    // the top of an iteration: DRAIN_STEP levels of the draining fold.  A lane whose fold completed in an
+    // earlier iteration and which holds a pending one starts that here: its slot is loaded with the levels
+    // (at the top of the iteration no store precedes the loads)
     auto drain_step = [&](uint32_t& dleft) {
-        uint32_t pos = lsu(VS_DPOS);
-        V3 L = ls3(VS_DL);
+        uint32_t pos, fid = 0;
+        V3 L;
+        bool act = false;
+        if (PEND && dleft == 0u) {
+            const uint32_t pd = lsu(VS_PEND);
+            const float4 meta = kargs4().stack_ld[pend_meta_at(pd)];
+            L = V3{meta.x, meta.y, meta.z};
+            fid = __float_as_uint(meta.w);
+            pos = pd & 0xFFFu;
+            dleft = pd >> 12;
+            act = true;
+            hasPend = false;
+        } else {
+            pos = lsu(VS_DPOS);
+            L = ls3(VS_DL);
+        }
         dleft -= fold_n(std::integral_constant<uint32_t, DRAIN_STEP>{}, pos, dleft, L);
+        if (PEND && act) {
+            lsu(VS_DT0) = lsu(VS_PLOC);
+            lsu(VS_DT1) = fid;
+        }
         if (dleft == 0u) {
             complete(L, lsu(VS_DT0), lsu(VS_DT1));
         } else {
@@ -354,14 +396,24 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             lsu(VS_DPOS) = pos;
         }
     };
-    // the rest of a draining fold at once (a path ended while the previous one still drains): the wave
-    // waits for one load latency per DRAIN_BATCH levels instead of one per level
+    // the rest of a draining fold at once: the wave waits for one load latency per DRAIN_BATCH levels instead
+    // of one per level; with PEND a pending fold is completed too
     auto drain_all = [&](uint32_t& dleft) {
-        if (dleft == 0u) return;
-        uint32_t pos = lsu(VS_DPOS);
-        V3 L = ls3(VS_DL);
-        while (dleft != 0u) dleft -= fold_n(std::integral_constant<uint32_t, DRAIN_BATCH>{}, pos, dleft, L);
-        complete(L, lsu(VS_DT0), lsu(VS_DT1));
+        if (dleft != 0u) {
+            uint32_t pos = lsu(VS_DPOS);
+            V3 L = ls3(VS_DL);
+            while (dleft != 0u) dleft -= fold_n(std::integral_constant<uint32_t, DRAIN_BATCH>{}, pos, dleft, L);
+            complete(L, lsu(VS_DT0), lsu(VS_DT1));
+        }
+        if (PEND && hasPend) {
+            const uint32_t pd = lsu(VS_PEND);
+            const float4 meta = kargs4().stack_ld[pend_meta_at(pd)];
+            V3 L = V3{meta.x, meta.y, meta.z};
+            uint32_t pos = pd & 0xFFFu, left = pd >> 12;
+            while (left != 0u) left -= fold_n(std::integral_constant<uint32_t, DRAIN_BATCH>{}, pos, left, L);
+            complete(L, lsu(VS_PLOC), __float_as_uint(meta.w));
+            hasPend = false;
+        }
     };
 
     // PRE (the leaf-box variant): camera rays are traced by the pre-pass (camera_prepass_kernel) and a path
@@ -525,8 +577,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             emissive = S.mats[2 * mat].w != 0.0f;
         }
         const bool ends = served && (PRE || pend) && (!cont || triA < 0 || emissive);
-        if (EXACT && __any(dleft != 0u)) {
-            if (dleft != 0u) drain_step(dleft);
+        if (EXACT && __any(dleft != 0u || hasPend)) {
+            if (dleft != 0u || hasPend) drain_step(dleft);
         }
         // (after the drain's ring loads are folded: the record's registers are then not live across them)
         uint32_t rid = NO_REC;
@@ -592,10 +644,17 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     if (pos >= R) pos -= R;
                     // the ring holds this path's levels above the draining ones, which occupy the R positions
                     // [dpos - dleft + 1, dpos]: a level must fit in the ring and not land on an undrained one
+                    // (with a pending fold behind the draining one, going up from here the draining levels come
+                    // first; between a fold's completion and the pending one's start, the pending levels and
+                    // their slot)
                     bool fits = lvl < R;
                     if (fits && dleft != 0u) {
                         const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
                         fits = (pos + R - lo) % R >= dleft;
+                    } else if (PEND && fits && hasPend) {
+                        const uint32_t pd = lsu(VS_PEND), pm = pd >> 12;
+                        const uint32_t lo = ((pd & 0xFFFu) + R + 1u - pm) % R;
+                        fits = (pos + R - lo) % R >= pm + 1u;
                     }
                     if (fits) {
                         if (Q.ring_pack) {
@@ -649,8 +708,32 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
                     const uint32_t m = (uint32_t)(fold_top + 1);
                     const uint32_t base = lsu(VS_BASE);
-                    drain_all(dleft);   // the previous sample's fold completes first
-                    if (m == 0u) {
+                    bool deferred = false;
+                    if (PEND && m != 0u && dleft != 0u && !hasPend) {
+                        // the previous fold still drains: this one waits behind it.  Its levels are ring positions
+                        // base .. base + m - 1; the slot above them takes (L, frame index) unless it would land on
+                        // the draining fold's undrained levels [lo, lo + dleft)
+                        const uint32_t R = Q.stack_depth;
+                        uint32_t top = base + m - 1u;
+                        if (top >= R) top -= R;
+                        uint32_t mp = top + 1u;
+                        if (mp >= R) mp -= R;
+                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
+                        if (m + 1u < R && (mp + R - lo) % R >= dleft) {
+                            Q.stack_ld[RING_AT(mp)] = make_float4(L.x, L.y, L.z, __uint_as_float(fidx));
+                            lsu(VS_PEND) = top | (m << 12);
+                            lsu(VS_PLOC) = local;
+                            hasPend = true;
+                            uint32_t nb = mp + 1u;
+                            if (nb >= R) nb -= R;
+                            lsu(VS_BASE) = nb;   // the next path pushes above the pending fold
+                            deferred = true;
+                        }
+                    }
+                    // (a one-vertex path has no level: its sample is parked now, whatever still drains)
+                    if (!deferred && !(PEND && m == 0u)) drain_all(dleft);   // the previous sample's fold completes first
+                    if (deferred) {
+                    } else if (m == 0u) {
                         complete(L, local, fidx);
                     } else {
                         // the fold drains from the innermost level, ring position base + m - 1
@@ -1462,7 +1545,9 @@ hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* m
 
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh)
 {
-    return (size_t)(lit ? (exact ? VS_WORDS_EXACT : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
+    // (the BVH variant keeps no pending fold: its two words stay unallocated unless the unlit RNG block follows)
+    const uint32_t exact_words = (bvh || RT_PEND_FOLD == 0) ? (uint32_t)VS_PEND : (uint32_t)VS_WORDS_EXACT;
+    return (size_t)(lit ? (exact ? exact_words : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
 }
 
 hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
