@@ -44,6 +44,7 @@ struct rt_ctx {
     // traffic): RT_RING_PACK 0 off, 1 BVH variant only, 2 both variants
     uint32_t ring_pack = 2;
     bool bvh_small_lds = true;   // RT_BVH_SMALL_LDS=0: the BVH variant reads materials and light tables from HBM
+    bool bvh_prepass = true;     // split scenes: the BVH variant's paths start from the camera pre-pass (RT_BVH_PREPASS=0: off)
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
@@ -426,6 +427,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_BVH_PREPASS")) c->bvh_prepass = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -468,7 +470,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
             c->occ_global[ex][cn] = b > 0 ? b : 2;
             if (ex) ex_max = std::max(ex_max, c->occ_global[ex][cn]);
         }
-    ex_max = std::max({ex_max, rt_coherent_occupancy(true, false, 256, 0), rt_coherent_occupancy(true, true, 256, 0)});
+    ex_max = std::max({ex_max, rt_coherent_occupancy(true, false, true, 256, 0), rt_coherent_occupancy(true, true, false, 256, 0),
+                       rt_coherent_occupancy(true, true, true, 256, 0)});
     c->block = 256;
     // the EXACT fold stack is sized for the largest grid any mode launches (LDS staging never
     // raises occupancy above the register-limited value)
@@ -736,13 +739,18 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.lds_scene_quads = lds ? (uint32_t)(lds_bytes / sizeof(float4)) : 0;
     // small scenes with decisive leaf boxes: the vertex-synchronous kernel (rt_coherent.hip)
     // any other path scene: its BVH variant, the scene in HBM (RT_VERTEX_BVH=0: the megakernel)
-    const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted;
+    // (the vertex kernel packs a material index in 14 bits beside the path's vertex count, rt_coherent.hip VS_MAT)
+    const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted && P.n_mats < (1u << 14);
     // (the camera pre-pass's records carry a triangle index in 19 bits, rt_kernels.h crec: only the leaf-box
     // variant runs the pre-pass, and its scenes have <= 64 triangles; the BVH variant carries full indices)
-    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31);
+    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31) &&
+                         P.n_mats < (1u << 14);
     const bool coh = coh_box || coh_bvh;
+    // the camera pre-pass: the leaf-box variant always; the BVH variant for a split scene, whose camera rays are
+    // traced like the path kernel's split phase (records carry the triangle in 19 bits, rt_kernels.h crec)
+    const bool prepass = coh_box || (coh_bvh && c->bvh_prepass && P.split_root != 0u && P.n_tris < (1u << 19));
     auto occupancy = [&](size_t bytes) {
-        return coh ? rt_coherent_occupancy(exact, coh_bvh, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
+        return coh ? rt_coherent_occupancy(exact, coh_bvh, prepass, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };
     const size_t lane_bytes = coh ? rt_coherent_lane_state_lds_bytes(exact, P.has_light != 0, coh_bvh) : rt_lane_state_lds_bytes(exact);
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
@@ -824,7 +832,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                 // frames rounded up to whole pre-pass segments of min(64, the next power of two) frames)
                 auto pass_bytes = [&](uint64_t nf) {
                     uint64_t b = 12ull * px_local * ((nf + 3) & ~3ull);
-                    if (coh_box) {
+                    if (prepass) {
                         uint64_t sf = 1;
                         while (sf < nf && sf < 64) sf <<= 1;
                         b += 16ull * items_px * ((nf + sf - 1) / sf * sf);
@@ -871,8 +879,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     c->kev.push_back(e);
                 }
                 HIPC(c, hipEventRecord(c->kev[3 * pass], c->stream));
-                if (coh_box) {
-                    // the leaf-box variant's camera pre-pass: segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
+                if (prepass) {
+                    // the camera pre-pass: segments of one 8x8 tile x F frames (F a power of two <= 64, rt_kernels.h crec)
                     Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
                     uint32_t lf = 0;
                     while ((1u << lf) < nf && lf < 6) ++lf;
@@ -918,10 +926,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.crec = c->d_crec; Q.ccount = c->d_ccount; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
                     Q.tile_boxes = c->d_tile_boxes;
                     Q.n_chunks = (uint32_t)(nseg / Q.n_tiles);
-                    HIPC(c, rt_launch_camera_prepass(Q, false, (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4), c->stream));
+                    const size_t pre_lds = coh_bvh ? (size_t)3 * P.n_split_leaves * sizeof(float4) : (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4);
+                    HIPC(c, rt_launch_camera_prepass(Q, coh_bvh, pre_lds, c->stream));
                 }
                 HIPC(c, hipEventRecord(c->kev[3 * pass + 1], c->stream));
-                if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, grid, c->block, shmem, c->stream));
+                if (coh) HIPC(c, rt_launch_coherent(Q, exact, coh_bvh, prepass, grid, c->block, shmem, c->stream));
                 else HIPC(c, rt_launch_megakernel(Q, exact, count, lds, grid, c->block, c->stream));
                 HIPC(c, hipEventRecord(c->kev[3 * pass + 2], c->stream));
                 // EXACT vertex kernel: the samples whose path outgrew the ring, rendered again into their
@@ -933,7 +942,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             }
             c->stats.n_passes = passes;
             c->kev_used = passes;
-            c->kev_prepass = coh_box;
+            c->kev_prepass = prepass;
         }
         c->stats.grid = grid;
         c->stats.kernel = whitted ? RT_KERNEL_WHITTED : (coh_bvh ? RT_KERNEL_VERTEX_BVH : coh ? RT_KERNEL_VERTEX : RT_KERNEL_MEGA);

@@ -44,7 +44,8 @@ enum : uint32_t {
     VS_LOCAL = 0,                        // the work item's local pixel
     VS_PIX = 1, VS_FRAME = 2,            // the sample's stream counter: global pixel y * W + x, frame number
     VS_LD = 3,                           // the pending vertex's unoccluded direct term (3 words)
-    VS_PCOS = 6, VS_MAT = 7,             // the pending vertex's indirect cosine and material
+    VS_PCOS = 6, VS_MAT = 7,             // the pending vertex's indirect cosine, and its material | the path's vertex
+                                         // count << VS_DEPTH_SHIFT (the count lives here, not in a register)
     VS_BASE = 8,                         // EXACT: ring position of the current path's level 0
     VS_DL = 9,                           // EXACT drain: the partial fold (3 words)
     VS_DPOS = 12,                        // EXACT drain: ring position of the next level to fold
@@ -57,6 +58,10 @@ enum : uint32_t {
     VS_RNG = 17,                         // unlit scenes only: the Philox block of the current 4 draws
     VS_WORDS_UNLIT = 21
 };
+
+// VS_MAT = material (< 2^14, host) | light-skip code << 14 (the sampled light triangle + 1 when its shadow-candidate
+// skip mask applies, 0 when not: read back by the trace of the same iteration) | the path's vertex count << 19
+constexpr uint32_t VS_SKIP_SHIFT = 14, VS_DEPTH_SHIFT = 19, VS_MAT_MASK = (1u << VS_SKIP_SHIFT) - 1u;
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
 // sample_hemisphere (straight-line code: the index folds to constants)
@@ -197,9 +202,13 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_COH_MIN_WAVES
 #define RT_COH_MIN_WAVES 8
 #endif
-// the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD
+// the BVH variant (scenes without decisive leaf boxes, e.g. C5): minimum waves per SIMD (without / with the
+// camera pre-pass)
 #ifndef RT_COH_BVH_MIN_WAVES
 #define RT_COH_BVH_MIN_WAVES 8
+#endif
+#ifndef RT_COH_BVH_PRE_MIN_WAVES
+#define RT_COH_BVH_PRE_MIN_WAVES 8
 #endif
 // section timing (diagnostic builds, tools/prof_one.py --sections / --hist; compiled by
 // tests/test_build_variants.py): wave cycles spent in fold drain (top) / vertex / finish / work queue +
@@ -253,8 +262,10 @@ struct GeneralSlab { static constexpr bool value = false; };
 // one after the other (A, then B) in the megakernel's rounds of `steps` box tests with up to two
 // postponed leaves, and a lane is served once both of its rays are done.
 // NARROW (leaf-box variant, <= 32 triangles): ray A's and ray B's candidates in the two halves of one mask.
-template <bool EXACT, bool BVH, bool NARROW>
-__global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
+// PREPASS: paths start at their first surface vertex from the camera pre-pass's records (the leaf-box variant
+// always; the BVH variant for split scenes, rt_capi.cpp), else the kernel traces the camera rays itself.
+template <bool EXACT, bool BVH, bool NARROW, bool PREPASS>
+__global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES : RT_COH_BVH_MIN_WAVES) : RT_COH_MIN_WAVES) pt_coherent_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
     SceneView S;
@@ -419,13 +430,12 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // PRE (the leaf-box variant): camera rays are traced by the pre-pass (camera_prepass_kernel) and a path
     // starts here at its first surface vertex; the BVH variant traces its camera rays itself (a pre-pass
     // cost it more than it saved, DESIGN.md 5.1: its time is in the secondary rays' BVH walks)
-    constexpr bool PRE = !BVH;
+    constexpr bool PRE = PREPASS;
     bool alive = true, in_path = false;
     bool have_pixel = false;   // !PRE: the lane holds a work item (frame chunk, pixel)
     uint32_t k = 0;            // !PRE: frame of the current item (item of chunk c: frames c * chunk_frames + [0, kend))
     bool pend = false;         // !PRE: the last vertex waits for its shadow verdict (false: the camera ray's hit)
     uint32_t pool_base = 0, pool_count = 0;   // !PRE: the wave's batch of work items (wave-uniform)
-    uint32_t depth = 0;   // vertices shaded so far on this path
     bool cont = false;    // the last vertex's roulette continued: ray A is its indirect ray
     VertexRng g;
     g.w = reinterpret_cast<uint32_t*>(lstate) + tib;
@@ -434,7 +444,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
-    uint32_t bskip = 0;                       // NARROW / split: shadow-ray candidates that cannot block (light plane)
     double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
     V3 hloc{0.f, 0.f, 0.f};                   // !BVH: ray A's hit location (from the trace) ...
     bool hflip = false;                       // ... and whether its normal faces away from -dA
@@ -453,7 +462,6 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
     uint32_t seg_pos = 0, seg_end = 0;
-    const uint32_t n_list = PRE ? __builtin_amdgcn_readfirstlane(*P.seg_list_n) << P.seg_part_shift : 0u;
     bool list_left = true;
 
 #if RT_SECTIONS
@@ -489,7 +497,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 uint32_t k = 0;
                 if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
                 k = __builtin_amdgcn_readfirstlane(k);
-                if (k >= n_list) { list_left = false; break; }
+                // (the list length is read here, once per segment, not kept live across the loop)
+                if (k >= (__builtin_amdgcn_readfirstlane(*Q.seg_list_n) << Q.seg_part_shift)) { list_left = false; break; }
                 // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records
                 const uint32_t ps = Q.seg_part_shift, part = k & ((1u << ps) - 1u);
                 const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k >> ps]);
@@ -570,6 +579,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
         // hit the light (radiance_indirect = 0, MC/Renderer.cpp:193-209).  They and the idle lanes take their
         // next sample now, so a finishing lane shades its next path's first vertex in the same iteration.
         const bool served = in_path && (!BVH || (tiA >= NN && tiB >= NN));
+        uint32_t depth = 0;   // vertices shaded so far on this path (from VS_MAT at the service; 0 for a new path)
         int mat = 0;
         bool emissive = false;
         if (served && hasA && triA >= 0) {
@@ -614,6 +624,8 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                 }
             } else {
                 // the last vertex's direct term (MC/Renderer.cpp:184-189): the shadow verdict
+                const uint32_t vmat = lsu(VS_MAT);
+                depth = vmat >> VS_DEPTH_SHIFT;
                 V3 ld{0.f, 0.f, 0.f};
                 if (hasB && !occB) ld = ls3(VS_LD);
                 if (!EXACT) {
@@ -625,7 +637,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     } else {
                         st3(VS_LSUM, lsum);
                         const float c = lsf(VS_PCOS);
-                        const float4 mb = S.mats[2 * lsu(VS_MAT)];
+                        const float4 mb = S.mats[2 * (vmat & VS_MAT_MASK)];
                         const V3 f = (c >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                         st3(VS_THR, muls(mul(thr, f), sdiv(sdiv(c, PDF, Q.y_pdf), Q.rr, Q.y_rr)));
                         vertex = true;
@@ -638,7 +650,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     // the indirect ray hit a surface: vertex depth-1 becomes stack level depth-1
                     const uint32_t lvl = depth - 1;
                     const float4 e = make_float4(ld.x, ld.y, ld.z, lsf(VS_PCOS));
-                    const uint32_t pm = lsu(VS_MAT);
+                    const uint32_t pm = vmat & VS_MAT_MASK;
                     const uint32_t R = Q.stack_depth;
                     uint32_t pos = lsu(VS_BASE) + lvl;
                     if (pos >= R) pos -= R;
@@ -813,12 +825,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             const V3 N{tq3.x, tq3.y, tq3.z};
             const V3 n = flip ? neg(N) : N;
             const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
+            uint32_t skipc = 0;
             auto shade = [&](auto& G) {
                 hasB = false;
                 if (Q.has_light) {
                     V3 q, nl0;
-                    uint32_t lskip = 0;
-                    sample_light(S, Q.light_area, G, q, nl0, &lskip);
+                    int lt = 0;
+                    sample_light(S, Q.light_area, G, q, nl0, nullptr, &lt);
                     const V3 p2q = sub(q, p);
                     const V3 wl = glm_normalize(p2q);
                     const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
@@ -840,14 +853,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                     // 0.006 + 2e-5 * extent of q along a shadow ray meeting the light at |cos| >= 0.25,
                     // so `slen < t + 0.01f` holds for them: they cannot block (host: rt_scene.cpp)
                     // (the BVH variant's split phase: the same masks over its outside slots, rt_scene.cpp)
-                    if ((NARROW && !BVH) || BVH) bskip = sc2 >= 0.25f ? lskip : 0u;
+                    // (the sampled light triangle is kept as the skip code in VS_MAT: the trace reads its mask back)
+                    if ((NARROW && !BVH) || BVH) skipc = (sc2 >= 0.25f && lt < 31) ? (uint32_t)lt + 1u : 0u;
                 }
                 // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
                 cont = G.next() < Q.rr && depth < 4096u;
                 if (cont) {
                     const V3 wi = glm_normalize(sample_hemisphere(n, G));
                     lsf(VS_PCOS) = dot(wi, n);
-                    lsu(VS_MAT) = (uint32_t)mat;
                     dA = wi;
                 }
             };
@@ -861,7 +874,7 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             hasA = cont;
             o = p;
             pend = true;
-            depth = depth + 1;
+            lsu(VS_MAT) = (uint32_t)mat | (skipc << VS_SKIP_SHIFT) | ((depth + 1u) << VS_DEPTH_SHIFT);
             if (BVH) {
                 tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
                 tA = 1.7976931348623157e308; triA = -1; occB = false;
@@ -958,7 +971,13 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
             }
             for (; b < nb; ++b) one_box(bx[b]);
         }
-        if (NARROW) { ca = ma; cb = mb & ~bskip; }
+        if (NARROW) {
+            // shadow-ray candidates that cannot block: the sampled light triangle's mask when the ray meets it at
+            // |cos| >= 0.25 (the skip code the vertex left in VS_MAT, rt_scene.cpp)
+            const uint32_t code = (lsu(VS_MAT) >> VS_SKIP_SHIFT) & 31u;
+            const uint32_t bskip = code != 0u ? __float_as_uint(S.ltris[4 * (code - 1u)].w) : 0u;
+            ca = ma; cb = mb & ~bskip;
+        }
         if (!trA || !fin) ca = 0;
         if (!trB || !fin) cb = 0;
         if (!fin && (trA || trB)) {
@@ -1133,8 +1152,10 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
                         if (box_hit_pk_within(sx, sy, sz, rB, bndB)) nB = root;
                     }
                     if (!okA) ma = 0u;
-                    mb = okB ? mb & ~bskip : 0u;   // outside slots near-coplanar with the sampled light triangle
-                    bskip = 0u;
+                    // outside slots near-coplanar with the sampled light triangle (its skip code in VS_MAT)
+                    const uint32_t code = (lsu(VS_MAT) >> VS_SKIP_SHIFT) & 31u;
+                    const uint32_t bskip = code != 0u ? __float_as_uint(S.ltris[4 * (code - 1u)].w) : 0u;
+                    mb = okB ? mb & ~bskip : 0u;
                     uint64_t cm = (uint64_t)ma | ((uint64_t)mb << 32);
                     while (cm != 0) {
                         const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
@@ -1279,12 +1300,14 @@ __global__ void __launch_bounds__(256, BVH ? RT_COH_BVH_MIN_WAVES : RT_COH_MIN_W
 #endif
 }
 
-template __global__ void pt_coherent_kernel<true, false, true>(KParams);
-template __global__ void pt_coherent_kernel<false, false, true>(KParams);
-template __global__ void pt_coherent_kernel<true, false, false>(KParams);
-template __global__ void pt_coherent_kernel<false, false, false>(KParams);
-template __global__ void pt_coherent_kernel<true, true, false>(KParams);
-template __global__ void pt_coherent_kernel<false, true, false>(KParams);
+template __global__ void pt_coherent_kernel<true, false, true, true>(KParams);
+template __global__ void pt_coherent_kernel<false, false, true, true>(KParams);
+template __global__ void pt_coherent_kernel<true, false, false, true>(KParams);
+template __global__ void pt_coherent_kernel<false, false, false, true>(KParams);
+template __global__ void pt_coherent_kernel<true, true, false, false>(KParams);
+template __global__ void pt_coherent_kernel<false, true, false, false>(KParams);
+template __global__ void pt_coherent_kernel<true, true, false, true>(KParams);
+template __global__ void pt_coherent_kernel<false, true, false, true>(KParams);
 
 // ---------------------------------------------------------------------------------------------
 // The vertex kernel's camera pre-pass.  One wave per segment (an 8x8 tile of local pixels x the segment's
@@ -1308,7 +1331,10 @@ template __global__ void pt_coherent_kernel<false, true, false>(KParams);
 // every ray of the tile.  Lane b tests box b in double; anything not finite keeps every box.
 __device__ __forceinline__ uint64_t tile_box_mask(const KParams& P, uint32_t lane, double px0, double px1, double py0, double py1)
 {
-    const uint32_t nb = P.n_lboxes;
+    // the leaf-box table of a small scene, or a split scene's outside boxes (rt_scene.cpp sboxes) with the walked
+    // subtree's root box as one more entry (bit n_sboxes)
+    const bool split = P.split_root != 0u;
+    const uint32_t nb = split ? P.n_sboxes + 1u : P.n_lboxes;
     // the rectangle's directions form a convex cone when the homogeneous w keeps one sign over it (a
     // perspective inverse: w does not depend on the pixel at all); otherwise nothing is culled
     int wsign = 0;
@@ -1329,7 +1355,14 @@ __device__ __forceinline__ uint64_t tile_box_mask(const KParams& P, uint32_t lan
               dirv(px0 - 1.0, py1 + 1.0, c[3]) && dirv(0.5 * (px0 + px1), 0.5 * (py0 + py1), m);
     bool keep = true;
     if (ok && lane < nb) {
-        const float* q = reinterpret_cast<const float*>(P.lboxes) + 8 * (size_t)lane;   // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, masks)
+        float q[6];
+        if (split && lane == P.n_sboxes) {   // the subtree root's node: (lo.xyz, hi.x)(hi.y, hi.z, skip, tri)
+            const float4 n0 = P.nodes[2 * P.split_root], n1 = P.nodes[2 * P.split_root + 1];
+            q[0] = n0.x; q[1] = n0.w; q[2] = n0.y; q[3] = n1.x; q[4] = n0.z; q[5] = n1.y;
+        } else {   // (lo.x, hi.x, lo.y, hi.y, lo.z, hi.z, masks)
+            const float* b = reinterpret_cast<const float*>(split ? P.sboxes : P.lboxes) + 8 * (size_t)lane;
+            for (int k = 0; k < 6; ++k) q[k] = b[k];
+        }
         const double lo[3] = {(double)q[0] - (double)P.cam_pos[0], (double)q[2] - (double)P.cam_pos[1], (double)q[4] - (double)P.cam_pos[2]};
         const double hi[3] = {(double)q[1] - (double)P.cam_pos[0], (double)q[3] - (double)P.cam_pos[1], (double)q[5] - (double)P.cam_pos[2]};
         for (int e = 0; e < 4 && keep; ++e) {
@@ -1368,6 +1401,37 @@ __global__ void __launch_bounds__(256) tile_boxes_kernel(KParams P)
     if (lane == 0) P.tile_boxes[tile] = m;
 }
 
+// The closest hit of a split scene's camera ray below the outside leaves' result (best, best_tri): the walk of
+// the subtree [root, end) in DFS pre-order with skip pointers (the reference's traversal restricted to the
+// subtree, whose root box lies inside every ancestor's, rt_scene.cpp), hit leaves postponed to one test per
+// round, boxes entered beyond the best hit skipped (exact: a triangle inside a box hits at t >= its entry,
+// the bound keeps 1e-5 relative margin), and the (min t, max DFS triangle) rule across both parts
+// (BVH::traverse_BVH_from_node's later-leaf-wins, MC/BVH.h:97-100).
+__device__ __forceinline__ void walk_subtree(const SceneView& S, const Ray& r, uint32_t root, uint32_t end, double& best, int& best_tri)
+{
+    uint32_t i = root;
+    while (i < end) {
+        const float bound = (best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff();
+        int parked = -1;
+        while (i < end) {
+            const float4 q0 = S.nodes[2 * i];
+            const float4 q1 = S.nodes[2 * i + 1];
+            const bool hit = slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound);
+            const int tri = f2i(q1.w);
+            i = (hit && tri < 0) ? i + 1 : (uint32_t)f2i(q1.z);
+            if (hit && tri >= 0) { parked = tri; break; }
+        }
+        if (parked >= 0) {
+            const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
+            double t;
+            if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t) &&
+                (t < best || (t == best && parked > best_tri))) {
+                best = t; best_tri = parked;
+            }
+        }
+    }
+}
+
 template <bool BVH>
 __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
 {
@@ -1382,6 +1446,16 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
         for (uint32_t i = threadIdx.x; i < mq; i += blockDim.x) dm[i] = P.mats[i];
         __syncthreads();
         S.tris = dt; S.mats = dm;
+    } else if (P.split_root != 0u) {
+        // a split scene: its <= 32 outside triangles by slot, as the path kernel stages them (a, e1, (e2, bits(triangle)))
+        for (uint32_t i = threadIdx.x; i < 3u * P.n_split_leaves; i += blockDim.x) {
+            const uint32_t k = i / 3u, j = i - 3u * k;
+            const int tri = P.stri[k];
+            float4 v = P.tris[4 * tri + j];
+            if (j == 2u) v.w = __int_as_float(tri);
+            lds_scene[i] = v;
+        }
+        __syncthreads();
     }
     const uint32_t lane = __lane_id();
     const uint32_t sg = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -1398,8 +1472,10 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
     const uint32_t nf = min(P.seg_frames, P.n_frames - f0);
     const V3 o{P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]};
     float4* const out = P.crec + ((size_t)sg << P.seg_shift);
-    // !BVH: the leaf boxes the tile's frustum meets (tile_boxes_kernel; wave-uniform)
-    const uint64_t boxes = BVH ? ~0ull : P.tile_boxes[tile];
+    // the leaf boxes (split scene: outside boxes + the subtree root) the tile's frustum meets (tile_boxes_kernel;
+    // wave-uniform)
+    const bool split = BVH && P.split_root != 0u;
+    const uint64_t boxes = (BVH && !split) ? ~0ull : P.tile_boxes[tile];
     uint32_t cnt = 0;
     for (uint32_t j = 0; j < nf; ++j) {
         const uint32_t fidx = f0 + j, frame = P.first_frame + fidx;
@@ -1447,10 +1523,47 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
                 if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, tk) && tk <= t) { t = tk; tri = k; }
             }
             fin = fin || !valid;
+        } else if (split) {
+            // the path kernel's split trace (rt_scene.cpp): the outside leaves by their own boxes, the subtree walked
+            // when its root box is hit; a box's own test decides whether the reference reaches it (leaf-box
+            // monotonicity), and the closest hit is taken by (min t, max DFS triangle)
+            uint32_t cm = 0;
+            const uint32_t ns = P.n_sboxes;
+            cbox8* bx = (cbox8*)P.sboxes;
+            const uint64_t bset = boxes & ((1ull << ns) - 1ull);
+            for (uint64_t bm = bset; bm != 0; bm &= bm - 1) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(bm);
+                const box8 q = bx[b];
+                const f2 sx = f2{q.s0, q.s1} - f2{o.x, o.x};
+                const f2 sy = f2{q.s2, q.s3} - f2{o.y, o.y};
+                const f2 sz = f2{q.s4, q.s5} - f2{o.z, o.z};
+                cm |= box_hit_pk(sx, sy, sz, r.rcp) ? (uint32_t)f2i(q.s6) : 0u;
+            }
+            bool walk = false;
+            if ((boxes >> ns) & 1ull) {
+                const float4 n0 = S.nodes[2 * P.split_root], n1 = S.nodes[2 * P.split_root + 1];
+                const f2 sx = f2{n0.x, n0.w} - f2{o.x, o.x};
+                const f2 sy = f2{n0.y, n1.x} - f2{o.y, o.y};
+                const f2 sz = f2{n0.z, n1.y} - f2{o.z, o.z};
+                walk = box_hit_pk(sx, sy, sz, r.rcp);
+            }
+            if (!valid || !fin) { cm = 0; walk = false; }
+            while (cm != 0) {
+                const uint32_t k = (uint32_t)__builtin_ctz(cm);
+                cm &= cm - 1;
+                const float4* T = lds_scene + 3u * k;
+                const float4 t0 = T[0], t1 = T[1], t2 = T[2];
+                const int kt = f2i(t2.w);
+                double tk;
+                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, tk) &&
+                    (tk < t || (tk == t && kt > tri))) { t = tk; tri = kt; }
+            }
+            if (walk) walk_subtree(S, r, P.split_root, P.split_end, t, tri);
+            fin = fin || !valid;
         } else {
             fin = __all(!valid || fin);
         }
-        if (valid && (BVH || !fin)) {
+        if (valid && ((BVH && !split) || !fin)) {
             // the BVH variant's scene, or a ray with a non-finite reciprocal direction: the stackless walk
             // (the reference's traversal, rt_path.h)
             bool occ = false;
@@ -1492,7 +1605,8 @@ hipError_t rt_launch_camera_prepass(const KParams& P, bool bvh, size_t lds, hipS
     if (P.n_segments == 0) return hipSuccess;
     const uint32_t blocks = (P.n_segments + 3u) / 4u;
     if (bvh) {
-        hipLaunchKernelGGL(camera_prepass_kernel<true>, dim3(blocks), dim3(256), 0, stream, P);
+        if (P.split_root != 0u) hipLaunchKernelGGL(tile_boxes_kernel, dim3((P.n_tiles + 3u) / 4u), dim3(256), 0, stream, P);
+        hipLaunchKernelGGL(camera_prepass_kernel<true>, dim3(blocks), dim3(256), lds, stream, P);
     } else {
         hipLaunchKernelGGL(tile_boxes_kernel, dim3((P.n_tiles + 3u) / 4u), dim3(256), 0, stream, P);
         hipLaunchKernelGGL(camera_prepass_kernel<false>, dim3(blocks), dim3(256), lds, stream, P);
@@ -1550,29 +1664,34 @@ size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh)
     return (size_t)(lit ? (exact ? exact_words : VS_WORDS_FAST) : VS_WORDS_UNLIT) * 256 * sizeof(float);
 }
 
-hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
+hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, bool prepass, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream)
 {
     const bool narrow = !bvh && P.n_tris <= 32;
-    if (bvh) {
-        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true, false>), dim3(grid), dim3(block), lds, stream, P);
-        else hipLaunchKernelGGL((pt_coherent_kernel<false, true, false>), dim3(grid), dim3(block), lds, stream, P);
+    if (bvh && prepass) {
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true, false, true>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, true, false, true>), dim3(grid), dim3(block), lds, stream, P);
+    } else if (bvh) {
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, true, false, false>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, true, false, false>), dim3(grid), dim3(block), lds, stream, P);
     } else if (narrow) {
-        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, true>), dim3(grid), dim3(block), lds, stream, P);
-        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, true>), dim3(grid), dim3(block), lds, stream, P);
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, true, true>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, true, true>), dim3(grid), dim3(block), lds, stream, P);
     } else {
-        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, false>), dim3(grid), dim3(block), lds, stream, P);
-        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, false>), dim3(grid), dim3(block), lds, stream, P);
+        if (exact) hipLaunchKernelGGL((pt_coherent_kernel<true, false, false, true>), dim3(grid), dim3(block), lds, stream, P);
+        else hipLaunchKernelGGL((pt_coherent_kernel<false, false, false, true>), dim3(grid), dim3(block), lds, stream, P);
     }
     return hipGetLastError();
 }
 
-int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes)
+int rt_coherent_occupancy(bool exact, bool bvh, bool prepass, int block, size_t lds_bytes)
 {
     int n = 0;
     hipError_t e;
-    if (bvh) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true, false>, block, lds_bytes)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true, false>, block, lds_bytes);
-    else e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, false, false>, block, lds_bytes)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, false, false>, block, lds_bytes);
+    if (bvh && prepass) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true, false, true>, block, lds_bytes)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true, false, true>, block, lds_bytes);
+    else if (bvh) e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, true, false, false>, block, lds_bytes)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, true, false, false>, block, lds_bytes);
+    else e = exact ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<true, false, false, true>, block, lds_bytes)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, pt_coherent_kernel<false, false, false, true>, block, lds_bytes);
     return e == hipSuccess ? n : 0;
 }

@@ -95,11 +95,12 @@ hipError_t rt_launch_megakernel(const KParams& P, bool exact, bool count, bool l
 int rt_megakernel_occupancy(bool exact, bool count, bool lds, int block, size_t lds_bytes);
 // the vertex-synchronous kernel (rt_coherent.hip; no counters, no G-buffer): small scenes (n_lboxes > 0,
 // scene in LDS: LDS = scene | lane state) or, bvh = true, any scene in HBM (LDS = lane state)
-hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
+hipError_t rt_launch_coherent(const KParams& P, bool exact, bool bvh, bool prepass, uint32_t grid, uint32_t block, size_t lds, hipStream_t stream);
 // its camera pre-pass: every sample's camera ray traced, misses / light hits parked, surface hits recorded
-// (KParams::crec); lds = the small scene's staged triangles + materials (0 for the BVH variant)
+// (KParams::crec); lds = the small scene's staged triangles + materials, or a split scene's staged outside
+// triangles (bvh: the BVH variant's pre-pass, for split scenes; prepass == true in rt_launch_coherent)
 hipError_t rt_launch_camera_prepass(const KParams& P, bool bvh, size_t lds, hipStream_t stream);
-int rt_coherent_occupancy(bool exact, bool bvh, int block, size_t lds_bytes);
+int rt_coherent_occupancy(bool exact, bool bvh, bool prepass, int block, size_t lds_bytes);
 size_t rt_coherent_lane_state_lds_bytes(bool exact, bool lit, bool bvh);
 // Whitted-style C3 renderer: one thread per local pixel, 16x16 tiles (grid_out: workgroups launched)
 hipError_t rt_launch_whitted(const KParams& P, bool count, hipStream_t stream, uint32_t* grid_out);

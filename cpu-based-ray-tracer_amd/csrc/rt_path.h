@@ -117,7 +117,7 @@ __device__ __forceinline__ void traverse(const SceneView& S, const Ray& r, bool 
 // SamplingAreaLight -> TriangleMesh::Sampling -> BVH::Sampling_from_root/_node -> TrianglePrimitive::Sampling
 // (MC/Renderer.h:163-180, MC/TriangleMesh.h:193-197, MC/BVH.h:103-129, MC/TriangleMesh.h:69-89)
 template <class G>
-__device__ __forceinline__ void sample_light(const SceneView& S, float light_area, G& g, V3& q, V3& nl, uint32_t* aw = nullptr)
+__device__ __forceinline__ void sample_light(const SceneView& S, float light_area, G& g, V3& q, V3& nl, uint32_t* aw = nullptr, int* lt_out = nullptr)
 {
     const float u0 = g.next();
     float p = u0 * light_area;
@@ -138,6 +138,7 @@ __device__ __forceinline__ void sample_light(const SceneView& S, float light_are
     q = add(add(smul(x, a), smul((1.0f - x) * y, b)), smul((1.0f - x) * (1.0f - y), c));
     nl = V3{N.x, N.y, N.z};
     if (aw) *aw = __float_as_uint(A.w);   // the light triangle's shadow-candidate skip mask (rt_layout.h ltris)
+    if (lt_out) *lt_out = lt;
 }
 
 // WhittedMaterial::Sampling, MC/WhittedMaterial.h:71-117
