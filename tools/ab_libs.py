@@ -59,20 +59,24 @@ def main():
         cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else (rt.camera_two_spheres(W, H) if args.scene == "c1" else rt.camera_default(W, H)[0])
         for k, _ in kv:
             os.environ.pop(k, None)
-        runs[spec] = (rt, ctx, cam, [], sc)
+        runs[spec] = (rt, ctx, cam, [], sc, [], [])
     kw = dict(whitted=True) if args.scene in ("c1", "c3") else dict(exact=not args.fast)
     ref = None
     for r in range(args.rounds + 1):
-        for name, (rt, ctx, cam, res, _) in runs.items():
+        for name, (rt, ctx, cam, res, _, pre, main) in runs.items():
             ctx.render(cam, spp, fetch=False, **kw)
             if r > 0:
-                res.append(W * H * spp / ctx.stats().last_kernel_ms / 1e3)
+                st = ctx.stats()
+                res.append(W * H * spp / st.last_kernel_ms / 1e3)
+                pre.append(st.last_prepass_ms)
+                main.append(st.last_main_ms)
     out = {}
-    for name, (rt, ctx, cam, res, _) in runs.items():
+    for name, (rt, ctx, cam, res, _, pre, main) in runs.items():
         _, acc = ctx.render(cam, 4, **kw)
         same = None if ref is None else bool(np.array_equal(acc.view(np.uint32), ref.view(np.uint32)))
         ref = acc if ref is None else ref
-        out[name] = {"median_msps": round(float(np.median(res)), 1), "grid": ctx.stats().grid, "bitwise_equal_to_first": same}
+        out[name] = {"median_msps": round(float(np.median(res)), 1), "grid": ctx.stats().grid, "bitwise_equal_to_first": same,
+                     "prepass_ms": round(float(np.median(pre)), 3), "path_kernel_ms": round(float(np.median(main)), 3)}
         ctx.close()
     print(json.dumps({"config": f"{W}x{H}x{spp} {args.scene} {'fast' if args.fast else 'exact'}", "libs": out}, indent=1))
 
