@@ -45,6 +45,7 @@ struct rt_ctx {
     uint32_t ring_pack = 2;
     bool bvh_small_lds = true;   // RT_BVH_SMALL_LDS=0: the BVH variant reads materials and light tables from HBM
     bool bvh_prepass = true;     // split scenes: the BVH variant's paths start from the camera pre-pass (RT_BVH_PREPASS=0: off)
+    bool pre_defer_walk = true;  // ... whose camera rays into the walked subtree are traced by the path kernel (RT_PRE_DEFER=0: walked there)
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
     rt_scene_header hdr{};
     bool has_scene = false;
@@ -428,6 +429,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_BVH_PREPASS")) c->bvh_prepass = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_PRE_DEFER")) c->pre_defer_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_CHUNKS")) c->force_chunks = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_ITEMS_PER_LANE")) c->items_per_lane = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
@@ -748,7 +750,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const bool coh = coh_box || coh_bvh;
     // the camera pre-pass: the leaf-box variant always; the BVH variant for a split scene, whose camera rays are
     // traced like the path kernel's split phase (records carry the triangle in 19 bits, rt_kernels.h crec)
-    const bool prepass = coh_box || (coh_bvh && c->bvh_prepass && P.split_root != 0u && P.n_tris < (1u << 19));
+    const bool prepass = coh_box || (coh_bvh && c->bvh_prepass && P.split_root != 0u && P.n_tris < (1u << 19) - 1u);
+    P.pre_defer_walk = c->pre_defer_walk ? 1u : 0u;
     auto occupancy = [&](size_t bytes) {
         return coh ? rt_coherent_occupancy(exact, coh_bvh, prepass, (int)c->block, bytes) : rt_megakernel_occupancy(exact, count, lds, (int)c->block, bytes);
     };

@@ -61,6 +61,9 @@ enum : uint32_t {
 
 // VS_MAT = material (< 2^14, host) | light-skip code << 14 (the sampled light triangle + 1 when its shadow-candidate
 // skip mask applies, 0 when not: read back by the trace of the same iteration) | the path's vertex count << 19
+// a camera-hit record's triangle field when the record is a camera ray left to the path kernel (its direction in
+// the location's place; the BVH variant's pre-pass, scenes of < 2^19 - 1 triangles)
+constexpr uint32_t CREC_CAMERA = 0x7FFFFu;
 constexpr uint32_t VS_SKIP_SHIFT = 14, VS_DEPTH_SHIFT = 19, VS_MAT_MASK = (1u << VS_SKIP_SHIFT) - 1u;
 
 // The six draws of a vertex of a lit scene, taken in order by sample_light / the roulette /
@@ -586,7 +589,9 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             mat = f2i(S.tris[4 * triA].w);
             emissive = S.mats[2 * mat].w != 0.0f;
         }
-        const bool ends = served && (PRE || pend) && (!cont || triA < 0 || emissive);
+        // (a path ends at a vertex's service; a camera ray's service is its hit: !PRE, or the BVH variant's camera
+        // rays the pre-pass left to it)
+        const bool ends = served && ((PRE && !BVH) || pend) && (!cont || triA < 0 || emissive);
         if (EXACT && __any(dleft != 0u || hasPend)) {
             if (dleft != 0u || hasPend) drain_step(dleft);
         }
@@ -610,7 +615,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             int fold_top = -1;   // EXACT: stack levels fold_top..0 are folded into L when the path ends
             bool relisted = false;   // EXACT: the sample went to the overflow list (no fold, no parked store)
             V3 L{0.f, 0.f, 0.f};
-            if (!PRE && !pend) {
+            if ((!PRE || BVH) && !pend) {
                 // the camera ray's hit (cast_path, MC/Renderer.cpp:136-146)
                 if (triA < 0) {   // miss: night sky (:145)
                     L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
@@ -791,14 +796,25 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             lsu(VS_PIX) = pix;
             lsu(VS_FRAME) = frame;
             g.start(pix, frame, !Q.has_light);   // the vertex draws continue after the 2 camera draws
-            loc = V3{rec.x, rec.y, rec.z};
-            tri = (int)(tag & 0x7FFFFu);
-            flip = (tag >> 31) != 0u;
-            mat = f2i(S.tris[4 * tri].w);
             depth = 0;
             in_path = true;
-            vertex = true;
             if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
+            if (BVH && (tag & CREC_CAMERA) == CREC_CAMERA) {
+                // a camera ray the pre-pass left to this kernel (it enters the walked subtree's box): traced here as a
+                // fresh ray A -- the split phase, then the walk in the rounds -- whose hit the next service takes
+                o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
+                dA = V3{rec.x, rec.y, rec.z};
+                hasA = true; hasB = false;
+                pend = false;
+                tiA = 0u; tiB = NN;
+                tA = 1.7976931348623157e308; triA = -1; occB = false;
+            } else {
+                loc = V3{rec.x, rec.y, rec.z};
+                tri = (int)(tag & 0x7FFFFu);
+                flip = (tag >> 31) != 0u;
+                mat = f2i(S.tris[4 * tri].w);
+                vertex = true;
+            }
 #if RT_SECTIONS
             dbg_cam = true;
 #endif
@@ -1498,6 +1514,7 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
         // closest hit, the later leaf winning ties (MC/BVH.h:97-100)
         double t = 1.7976931348623157e308;
         int tri = -1;
+        bool deferred = false;   // (split scenes) the ray is left to the path kernel
         bool fin = rcp_finite(r) && P.force_walk == 0u;
         if (!BVH) {
             // the distinct leaf boxes decide the candidates (rt_scene.cpp); Moller-Trumbore in DFS order
@@ -1548,6 +1565,7 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
                 walk = box_hit_pk(sx, sy, sz, r.rcp);
             }
             if (!valid || !fin) { cm = 0; walk = false; }
+            if (walk && P.pre_defer_walk) { deferred = true; cm = 0; walk = false; }   // the path kernel traces it
             while (cm != 0) {
                 const uint32_t k = (uint32_t)__builtin_ctz(cm);
                 cm &= cm - 1;
@@ -1573,7 +1591,11 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
         }
         bool surface = false;
         float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (valid) {
+        if (deferred) {
+            // a camera ray entering the walked subtree's box: a record of its direction, traced by the path kernel
+            surface = true;
+            rec = make_float4(d.x, d.y, d.z, __uint_as_float(CREC_CAMERA | (lane << 19) | (j << 25)));
+        } else if (valid) {
             V3 L{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};   // cast_path miss: night sky (MC/Renderer.cpp:145)
             if (tri >= 0) {
                 const int mat = f2i(S.tris[4 * tri].w);

@@ -71,6 +71,10 @@ struct KParams {
     // pass with few tiles keeps long pre-pass segments and still hands out fine-grained work
     float4* crec; uint32_t* ccount; uint32_t* seg_list; uint32_t* seg_list_n;
     unsigned long long* tile_boxes;   // per tile: the leaf boxes its camera rays' frustum meets (tile_boxes_kernel)
+    // split scenes (the BVH variant's pre-pass): a camera ray that enters the walked subtree's box is recorded as a
+    // camera ray (triangle field CREC_CAMERA, its direction in the location's place) and traced by the path kernel,
+    // instead of walked here (0: the pre-pass walks it)
+    uint32_t pre_defer_walk;
     uint32_t n_segments, n_tiles, seg_frames, seg_shift, seg_part_shift;
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
