@@ -207,9 +207,11 @@ __device__ __forceinline__ bool moller_trumbore_od(const V3& a, const V3& e1, co
     const V3 S1 = cross(d, e2), S2 = cross(S, e1);
     const float den = dot(S1, e1);
     const float tn = dot(S2, e2), b2n = dot(S1, S), b3n = dot(S2, d);
-    const bool pos = (tn > 0.0f) && (b2n > 0.0f) && (b3n > 0.0f);
-    const bool ngt = (tn < 0.0f) && (b2n < 0.0f) && (b3n < 0.0f);
-    if (!(pos || ngt)) return false;
+    // tn, b2n, b3n share one strict sign (v_min3 / v_max3 instead of six compares and their mask logic).  A NaN
+    // among them is dropped by min/max, where the compares failed at once -- the outcome is the same: a NaN
+    // tn, b2n or den reaches the double stage as a NaN t or b2 and `t > 0.0` / `(1 - b2) - b3 > 0.0` fail
+    const float lo3 = __builtin_fminf(__builtin_fminf(tn, b2n), b3n), hi3 = __builtin_fmaxf(__builtin_fmaxf(tn, b2n), b3n);
+    if (!(lo3 > 0.0f || hi3 < 0.0f)) return false;
     const float sb = __builtin_fabsf(b2n) + __builtin_fabsf(b3n), aden = __builtin_fabsf(den);
     if (sb > aden * 1.00001f) return false;
     const double inv = rcp_f64_of_f32(den);   // == 1.0 / (double)den
