@@ -211,7 +211,7 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #define RT_COH_BVH_MIN_WAVES 8
 #endif
 #ifndef RT_COH_BVH_PRE_MIN_WAVES
-#define RT_COH_BVH_PRE_MIN_WAVES 8
+#define RT_COH_BVH_PRE_MIN_WAVES 7
 #endif
 // section timing (diagnostic builds, tools/prof_one.py --sections / --hist; compiled by
 // tests/test_build_variants.py): wave cycles spent in fold drain (top) / vertex / finish / work queue +

@@ -51,9 +51,11 @@ def flops_per_sample(c):
     return r * (n * 18 + t * 54) + 0.4036 * r * 150
 
 
-def run(ctx, cam, W, H, spp, reps, **kw):
+def run(ctx, cam, W, H, spp, reps, full_warmup=False, **kw):
     ctx.resize(W, H)
-    ctx.render(cam, min(spp, 8), fetch=False, **kw)   # warm-up
+    # warm-up; a render longer than the warm-up allocates its parked-sample and camera-record buffers
+    # (tens of GB at C5 4096 spp) inside its first timed call unless the warm-up renders the full spp
+    ctx.render(cam, spp if full_warmup else min(spp, 8), fetch=False, **kw)
     ms = []
     for _ in range(reps):
         ctx.render(cam, spp, fetch=False, **kw)
@@ -67,6 +69,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--c5-spp", type=int, default=64)
     ap.add_argument("--fast", action="store_true")
+    ap.add_argument("--full-warmup", action="store_true", help="warm up at the measured spp (steady-state buffers)")
     args = ap.parse_args()
     bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
     for c in args.configs.split(","):
@@ -121,7 +124,7 @@ def main():
             kw = dict(exact=not args.fast)
         else:
             raise SystemExit(f"unknown config {c}")
-        ms = run(ctx, cam, W, H, spp, args.reps, **kw)
+        ms = run(ctx, cam, W, H, spp, args.reps, full_warmup=args.full_warmup, **kw)
         st = ctx.stats()
         samples = W * H * spp
         rate = samples / (ms / 1e3)
@@ -129,7 +132,8 @@ def main():
         roof = None if fps is None else {"bound": "valu", "flops_per_sample": round(fps, 1), "achieved_tflops": round(fps * rate / 1e12, 3),
                                          "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(fps * rate / 1e12 / VALU_PEAK_TFLOPS, 4)}
         print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
-                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "roofline": roof,
+                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "passes": st.n_passes,
+                          "prepass_ms": round(st.last_prepass_ms, 3), "path_ms": round(st.last_main_ms, 3), "roofline": roof,
                           "mode": "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")}), flush=True)
         ctx.close()
 

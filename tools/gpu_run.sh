@@ -8,12 +8,12 @@
 #   smoke                  __graft_entry__.smoke()                                -> smoke.log
 #   bench                  the default bench line (C4, N = 1)                     -> bench.log
 #   configs                C1..C5 and the denoiser (tools/bench_configs.py)       -> configs.jsonl
-#   c5full                 C5 at its full 4096 spp                                -> c5_4096.jsonl
+#   c5full                 C5 at its full 4096 spp (warm-up at 4096 spp)                            -> c5_4096.jsonl
 #   prof                   rocprofv3 trace + PMC passes of the bench command      -> profiles via profiles/run_rocprof.sh
 #   profc5                 the same for C5 at 64 spp                              -> tools/prof_c5.sh
 #   ab:ARGS                tools/ab_libs.py ARGS (comma-separated, e.g. ab:librt_hip.so,librt_hip_x.so,--spp,256)
 #   sweep:ARGS             tools/sweep_env.py ARGS (comma-separated)
-#   sections:LIB:SCENE:SPP wave cycles per kernel section of an RT_SECTIONS build (tools/prof_one.py)
+#   sections:LIB:SCENE:SPP[:W:H] wave cycles per kernel section of an RT_SECTIONS build (tools/prof_one.py)
 #
 #   gpurun --timeout 1200 -- 'bash tools/gpu_run.sh r04a tests smoke bench prof'
 set -euo pipefail
@@ -47,7 +47,7 @@ for step in "$@"; do
       timeout -k 10 400 python3 -u tools/bench_configs.py > "$OUT/configs.jsonl" 2> "$OUT/configs.err"
       cut -c1-300 "$OUT/configs.jsonl" ;;
     c5full)
-      timeout -k 10 300 python3 -u tools/bench_configs.py --configs C5 --c5-spp 4096 --reps 1 > "$OUT/c5_4096.jsonl" 2>> "$OUT/configs.err"
+      timeout -k 10 300 python3 -u tools/bench_configs.py --configs C5 --c5-spp 4096 --reps 1 --full-warmup > "$OUT/c5_4096.jsonl" 2>> "$OUT/configs.err"
       cat "$OUT/c5_4096.jsonl" ;;
     prof)
       bash profiles/run_rocprof.sh "$TAG" ;;
@@ -62,8 +62,9 @@ for step in "$@"; do
       timeout -k 10 400 python3 -u tools/sweep_env.py "${a[@]}" > "$OUT/sweep_$n.json" 2>&1 || { tail -20 "$OUT/sweep_$n.json"; exit 1; }
       cat "$OUT/sweep_$n.json" ;;
     sections:*)
-      IFS=':' read -r _ lib scene spp <<< "$step"
-      timeout -k 10 200 python3 tools/prof_one.py "$lib" --sections --scene "$scene" --spp "$spp" > "$OUT/sections_${scene}_${spp}spp.txt" 2>&1
+      IFS=':' read -r _ lib scene spp w h <<< "$step"
+      timeout -k 10 200 python3 tools/prof_one.py "$lib" --sections --scene "$scene" --spp "$spp" --width "${w:-1920}" --height "${h:-1080}" \
+        > "$OUT/sections_${scene}_${spp}spp.txt" 2>&1
       cat "$OUT/sections_${scene}_${spp}spp.txt" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
