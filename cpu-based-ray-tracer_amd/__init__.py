@@ -124,6 +124,7 @@ def lib():
         "rt_upload_scene": (i32, [vp, vp]),
         "rt_upload_scene_gpu_bvh": (i32, [vp, vp, fp]),
         "rt_scene_lbvh_host": (i32, [vp, fp, fp]),
+        "rt_scene_walk_orders": (i32, [vp, fp, C.POINTER(C.c_uint64)]),
         "rt_debug_scene_arrays": (i32, [vp, fp, u32, fp, u32]),
         "rt_resize": (i32, [vp, u32, u32, u32, u32, u32]),
         "rt_local_rows": (u32, [vp]),
@@ -296,6 +297,17 @@ class Scene:
         nodes = np.zeros((2 * n - 1, 8), np.float32); tris = np.zeros((n, 16), np.float32)
         self._check(lib().rt_scene_lbvh_host(self.h, _fp(nodes), _fp(tris)), "rt_scene_lbvh_host")
         return nodes, tris
+
+    def walk_orders(self):
+        """The split subtree's 8 near-first pre-orders (rt_scene_walk_orders): (8, split_end - split_root, 8)
+        float32 in the traversal layout, or None when the scene has no split."""
+        n = C.c_uint64(0)
+        self._check(lib().rt_scene_walk_orders(self.h, None, C.byref(n)), "rt_scene_walk_orders")
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, np.float32)
+        self._check(lib().rt_scene_walk_orders(self.h, _fp(out), C.byref(n)), "rt_scene_walk_orders")
+        return out.reshape(8, -1, 8)
 
     def export(self):
         i = self.info()

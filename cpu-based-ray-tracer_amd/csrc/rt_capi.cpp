@@ -35,6 +35,7 @@ struct rt_ctx {
     float4 *d_nodes = nullptr, *d_tris = nullptr, *d_mats = nullptr, *d_lnodes = nullptr, *d_ltris = nullptr, *d_lboxes = nullptr;
     float4* d_sboxes = nullptr;   // split trace (FlatScene::sboxes): outside leaf boxes
     int32_t* d_stri = nullptr;    // split trace: outside slot -> triangle
+    float4* d_wcopies = nullptr;  // split trace: near-first orderings of the walked subtree (FlatScene::wcopies)
     uint32_t split_root = 0, split_end = 0, n_sboxes = 0, n_sleaves = 0;
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
@@ -112,6 +113,7 @@ struct rt_ctx {
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
     bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
+    bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
@@ -407,6 +409,15 @@ rt_status rt_scene_export(const rt_scene* s, float* nf, int32_t* ni, float* tf, 
     return RT_OK;
 }
 
+rt_status rt_scene_walk_orders(const rt_scene* s, float* out, uint64_t* n_floats)
+{
+    if (!s || !s->built) return RT_ERR_STATE;
+    if (!n_floats) return RT_ERR_INVALID;
+    *n_floats = s->flat.wcopies.size();
+    if (out && !s->flat.wcopies.empty()) std::memcpy(out, s->flat.wcopies.data(), s->flat.wcopies.size() * sizeof(float));
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ context
 rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
 {
@@ -421,6 +432,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
@@ -488,7 +500,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_sboxes); dfree(c->d_stri);
+    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_lboxes); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
     dfree(c->d_went); dfree(c->d_wtris);
@@ -524,6 +536,7 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_lboxes, s->flat.lboxes)) != RT_OK) return r;
     if ((r = upload(c, c->d_sboxes, s->flat.sboxes)) != RT_OK) return r;
     if ((r = upload(c, c->d_stri, s->flat.stri)) != RT_OK) return r;
+    if ((r = upload(c, c->d_wcopies, s->flat.wcopies)) != RT_OK) return r;
     c->split_root = s->flat.split_root;
     c->split_end = s->flat.split_end;
     c->n_sboxes = (uint32_t)(s->flat.sboxes.size() / 8);
@@ -607,7 +620,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     c->d_nodes = d_nodes; c->d_tris = d_tris;
     // the BVH-walking kernels: no leaf-box table, no compact tree
     dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
-    dfree(c->d_sboxes); dfree(c->d_stri);   // the split refers to the host tree's node order
+    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies);   // the split refers to the host tree's node order
     c->split_root = c->split_end = c->n_sboxes = c->n_sleaves = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
@@ -688,6 +701,12 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (c->split && c->split_root != 0 && P.n_lboxes == 0) {
         P.sboxes = c->d_sboxes; P.stri = c->d_stri; P.n_sboxes = c->n_sboxes;
         P.split_root = c->split_root; P.split_end = c->split_end; P.n_split_leaves = c->n_sleaves;
+        // (not with the compact tree or the forced full walk: both walk the original order)
+        if (c->walk_order && c->d_wcopies && !c->qbvh && !c->force_walk) {
+            // offset so that node k of an ordering is at [2 * k] (k >= split_root; computed as an integer)
+            P.wcopies = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(c->d_wcopies) - (uintptr_t)c->split_root * 2u * sizeof(float4));
+            P.wcopy_stride = 2u * (c->split_end - c->split_root);
+        }
     }
     P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
     P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;

@@ -447,7 +447,12 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
     V3 o{0.f, 0.f, 0.f}, dA{0.f, 0.f, 1.f}, rA{0.f, 0.f, 1.f}, dB{0.f, 0.f, 1.f}, rB{0.f, 0.f, 1.f};
     bool hasA = false, hasB = false;
     float slen = 0.0f;                        // length(q - p) of the shadow ray
-    double tA = 1.7976931348623157e308;       // closest t (DBL_MAX = IntersectionRecord default)
+    // closest t: the reference's IntersectionRecord default is DBL_MAX.  The BVH variant starts from +inf
+    // instead, an inline constant (DBL_MAX is a 64-bit literal the register allocator spilled): every t the
+    // intersection yields is +inf or at most FLT_MAX * 2^149 (a float over a float's double reciprocal), so
+    // `t < tA` is the same test, and a tie at +inf is refused by the unsigned triangle compare (triA = -1)
+    constexpr double TA_NONE = BVH ? __builtin_inf() : 1.7976931348623157e308;
+    double tA = TA_NONE;
     V3 hloc{0.f, 0.f, 0.f};                   // !BVH: ray A's hit location (from the trace) ...
     bool hflip = false;                       // ... and whether its normal faces away from -dA
     int triA = -1;                            // closest triangle
@@ -807,7 +812,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 hasA = true; hasB = false;
                 pend = false;
                 tiA = 0u; tiB = NN;
-                tA = 1.7976931348623157e308; triA = -1; occB = false;
+                tA = TA_NONE; triA = -1; occB = false;
             } else {
                 loc = V3{rec.x, rec.y, rec.z};
                 tri = (int)(tag & 0x7FFFFu);
@@ -893,7 +898,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             lsu(VS_MAT) = (uint32_t)mat | (skipc << VS_SKIP_SHIFT) | ((depth + 1u) << VS_DEPTH_SHIFT);
             if (BVH) {
                 tiA = hasA ? 0u : NN; tiB = hasB ? 0u : NN;
-                tA = 1.7976931348623157e308; triA = -1; occB = false;
+                tA = TA_NONE; triA = -1; occB = false;
             }
         }
 
@@ -923,7 +928,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             in_path = true;
             if (BVH) {
                 tiA = 0u; tiB = NN;
-                tA = 1.7976931348623157e308; triA = -1; occB = false;
+                tA = TA_NONE; triA = -1; occB = false;
             }
             if (!EXACT) { st3(VS_THR, V3{1.0f, 1.0f, 1.0f}); st3(VS_LSUM, V3{0, 0, 0}); }
         }
@@ -946,7 +951,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         // ======================= trace both rays of every lane =======================
         if (!BVH) {
         const bool trA = in_path && hasA, trB = in_path && hasB;
-        tA = 1.7976931348623157e308; triA = -1; occB = false;
+        tA = TA_NONE; triA = -1; occB = false;
         // the reciprocal directions are computed here, not when the rays are set up: they are then
         // temporaries of the box loop instead of 6 registers live across the iteration
         rA = rcp3(dA); rB = rcp3(dB);
@@ -1184,7 +1189,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         double t;
                         if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, useA ? dA : dB, t)) {
                             if (useA) {
-                                if (t < tA || (t == tA && tri > triA)) { tA = t; triA = tri; }
+                                if (t < tA || (t == tA && (uint32_t)tri > (uint32_t)triA)) { tA = t; triA = tri; }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 nB = NN;
@@ -1248,9 +1253,14 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         }
                     };
                     auto walk = [&](auto kind) {
+                        // a split scene's ray with a finite reciprocal direction walks the subtree from its root:
+                        // in the near-first ordering of its direction's octant when the scene has them
+                        const float4* wn = S.nodes;
+                        if (Q.wcopies != nullptr && (decltype(kind)::value || finite3(r.rcp)))
+                            wn = Q.wcopies + ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) * Q.wcopy_stride;
                         for (uint32_t s = 0; s < steps && ti < NN; ++s) {
-                            const float4 q0 = S.nodes[2 * ti];
-                            const float4 q1 = S.nodes[2 * ti + 1];
+                            const float4 q0 = wn[2 * ti];
+                            const float4 q1 = wn[2 * ti + 1];
                             const bool hit = decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
                                                                    : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                             const int tri = f2i(q1.w);
@@ -1292,7 +1302,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             if (curA) {
                                 // the later leaf wins ties (MC/BVH.h:97-100): triangles are numbered in DFS order,
                                 // and the split trace's outside leaves are tested first
-                                if (t < tA || (t == tA && pk > triA)) { tA = t; triA = pk; }
+                                if (t < tA || (t == tA && (uint32_t)pk > (uint32_t)triA)) { tA = t; triA = pk; }
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 ti = NN;

@@ -18,6 +18,9 @@ struct KParams {
     // split trace (larger scenes, the vertex kernel's BVH variant; rt_scene.h FlatScene::sboxes): the rays walk
     // only the subtree [split_root, split_end), the outside leaves are tested by their boxes (split_root = 0: off)
     const float4* sboxes; const int32_t* stri; uint32_t n_sboxes, split_root, split_end, n_split_leaves;
+    // the subtree's near-first orderings (rt_scene.h FlatScene::wcopies; null: off): ordering o's node k at
+    // wcopies[2 * k + o * wcopy_stride], k in [split_root, split_end) (the pointer is offset by -2 * split_root)
+    const float4* wcopies; uint32_t wcopy_stride;
     uint32_t lds_small;   // the BVH variant: the small tables (mats | lnodes | ltris) are staged in LDS; the split's
                           // outside triangles (3 float4 per slot: a, e1, (e2, bits(triangle))) follow them
     // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex

@@ -446,6 +446,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     // box must contain the leaf box), and the subtree is walked from its root, whose box must likewise lie
     // inside every ancestor's: then the root's own slab test decides whether the reference enters it.
     out.sboxes.clear();
+    out.wcopies.clear();
     out.stri.clear();
     out.split_root = out.split_end = 0;
     if (NT > 64) {
@@ -487,6 +488,44 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             out.split_root = r;
             out.split_end = rend;
             out.stri = slots;
+            // near-first orderings of the walked subtree, one per direction octant (bit 0: d.x < 0, bit 1: d.y,
+            // bit 2: d.z): the same nodes in the pre-order that visits, at every internal node, first the child
+            // whose box centre lies nearer along the axis that separates the two centres most.  A walk stops
+            // at the subtree's end (its skip pointers reach split_end only when it is done: stored as NN).
+            // Exact in any order: the kernel keeps the closest hit by (min t, max DFS triangle) and a box
+            // entered beyond it is skipped, and a shadow ray's verdict is any blocking hit.
+            const uint32_t M = rend - r;
+            out.wcopies.assign((size_t)8 * M * 8, 0.0f);
+            auto centre = [](const Box& b, int a) { return a == 0 ? b.lo.x + b.hi.x : a == 1 ? b.lo.y + b.hi.y : b.lo.z + b.hi.z; };
+            std::vector<uint32_t> st;
+            for (uint32_t oct = 0; oct < 8; ++oct) {
+                float* base = &out.wcopies[(size_t)oct * M * 8];
+                uint32_t pos = 0;
+                st.assign(1, r);
+                while (!st.empty()) {
+                    const uint32_t i = st.back();
+                    st.pop_back();
+                    const FN& n = fn[i];
+                    const uint32_t size = (uint32_t)n.skip - i;   // the subtree of i is [i, skip) in the DFS order
+                    uint32_t sk = r + pos + size;
+                    if (sk >= rend) sk = NN;
+                    float* q = base + 8 * (size_t)pos++;
+                    q[0] = n.box.lo.x; q[1] = n.box.lo.y; q[2] = n.box.lo.z; q[3] = n.box.hi.x;
+                    q[4] = n.box.hi.y; q[5] = n.box.hi.z; q[6] = bits_as_float((int32_t)sk); q[7] = bits_as_float(n.tri);
+                    if (n.tri >= 0) continue;
+                    const uint32_t a = i + 1, b = (uint32_t)fn[a].skip;   // left child, right child
+                    int ax = 0;
+                    float best = -1.0f;
+                    for (int k = 0; k < 3; ++k) {
+                        const float dk = std::fabs(centre(fn[a].box, k) - centre(fn[b].box, k));
+                        if (dk > best) { best = dk; ax = k; }
+                    }
+                    const bool neg = ((oct >> ax) & 1u) != 0u;
+                    const bool a_first = (centre(fn[a].box, ax) <= centre(fn[b].box, ax)) != neg;
+                    st.push_back(a_first ? b : a);
+                    st.push_back(a_first ? a : b);
+                }
+            }
             out.sboxes.resize(uniq.size() * 8);
             for (size_t k = 0; k < uniq.size(); ++k) {
                 const Box& b = uniq[k].first;

@@ -55,6 +55,9 @@ struct FlatScene {
     std::vector<float> sboxes;
     std::vector<int32_t> stri;
     uint32_t split_root = 0, split_end = 0;
+    // split scenes: the walked subtree in 8 near-first pre-orders (one per direction octant), the nodes
+    // layout, node k of ordering o at [(o * (split_end - split_root) + k) * 8], indices as in `nodes`
+    std::vector<float> wcopies;
     std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
     std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag

@@ -122,6 +122,11 @@ rt_status rt_scene_export(const rt_scene* s, float* node_f, int32_t* node_i, flo
  * a Karras LBVH over the Morton codes of the triangle-box centroids, one triangle per leaf, in the
  * traversal layout -- nodes: 8 floats x (2 n_tris - 1), tris: 16 floats x n_tris.  Needs >= 2 triangles. */
 rt_status rt_scene_lbvh_host(const rt_scene* s, float* nodes, float* tris);
+/* A split scene's walked subtree in its 8 near-first pre-orders (one per ray-direction octant, bit 0 = d.x < 0,
+ * bit 1 = d.y < 0, bit 2 = d.z < 0), for tests: 8 x (split_end - split_root) nodes of 8 floats in the traversal
+ * layout (indices as in the DFS order; a skip pointer that leaves the subtree reads n_nodes).  *n_floats
+ * receives the size (0: no split); out may be null to query it. */
+rt_status rt_scene_walk_orders(const rt_scene* s, float* out, uint64_t* n_floats);
 
 /* ------------------------------------------------------------------ camera (host math) */
 typedef struct {

@@ -163,7 +163,7 @@ def test_full_frame_digest(ctx, fixture):
 @pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"},
                                  {"RT_BVH_SMALL_LDS": "0"}, {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_THRESH": "0", "RT_STEPS": "1"},
                                  {"RT_THRESH": "64"}, {"RT_BVH_PREPASS": "0"}, {"RT_BVH_PREPASS": "0", "RT_FORCE_WALK": "1"},
-                                 {"RT_PRE_DEFER": "0"}])
+                                 {"RT_PRE_DEFER": "0"}, {"RT_WALK_ORDER": "0"}, {"RT_WALK_ORDER": "0", "RT_BVH_PREPASS": "0"}])
 def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):
     """The vertex kernel's BVH variant (the C5 path) on the reference's 96x54x16 accumulation, with the
     fold-level materials in their own array or in the direct term's sign bits, walking the exact
@@ -173,8 +173,10 @@ def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):
     and traced by the path kernel, RT_PRE_DEFER=0: walked by the pre-pass) or by the path kernel itself
     (RT_BVH_PREPASS=0).  The split trace (default:
     the 32 Cornell leaves by their boxes, the bunny's subtree walked; closest hit by (min t, max
-    triangle)) against the whole-tree walk (RT_SPLIT=0), the reference's per-lane traversal for every
-    ray (RT_FORCE_WALK=1: the split's non-finite-direction path), and extreme round shapes"""
+    triangle); the subtree walked in the near-first ordering of the ray's direction octant, or in the
+    reference's DFS order with RT_WALK_ORDER=0) against the whole-tree walk (RT_SPLIT=0), the reference's
+    per-lane traversal for every ray (RT_FORCE_WALK=1: the split's non-finite-direction path), and extreme
+    round shapes"""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     c = rt.Context(0)

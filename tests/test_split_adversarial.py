@@ -96,7 +96,8 @@ def test_split_bound_fails_no_mask():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("far", [False, True])
-@pytest.mark.parametrize("env", [{}, {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_BVH_PREPASS": "0"}, {"RT_PRE_DEFER": "0"}])
+@pytest.mark.parametrize("env", [{}, {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_BVH_PREPASS": "0"}, {"RT_PRE_DEFER": "0"},
+                                 {"RT_WALK_ORDER": "0"}])
 def test_split_adversarial_matches_oracle(far, env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)

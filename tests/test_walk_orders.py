@@ -1,0 +1,119 @@
+"""The split trace's near-first walk orders (rt_scene.cpp FlatScene::wcopies, rt_scene_walk_orders; DESIGN.md
+5.1), on the CPU.
+
+A split scene's walked subtree is stored in 8 pre-orders, one per ray-direction octant, each visiting the
+nearer child first.  The kernel walks them stacklessly (hit: next node, miss or leaf: the node's skip
+pointer) and ends when the pointer reads n_nodes.  The GPU tests check the images bitwise
+(test_c5.py, test_split_adversarial.py); these check the tables themselves: every ordering holds the
+subtree's nodes exactly once, its skip pointers describe a well-formed pre-order that ends at n_nodes, and a
+walk under any box predicate reaches the same leaves as the reference's DFS walk of the subtree -- the
+kernel keeps the closest hit by (min t, max DFS triangle), so the visit order does not change its result."""
+import numpy as np
+import pytest
+
+import test_split_adversarial as SA
+from _rt import rt
+
+
+def original(sc):
+    """the DFS pre-order's nodes as (boxes (n, 6), skip (n,), tri (n,)) from rt_scene_export"""
+    nf, ni, _, _ = sc.export()
+    n = len(nf)
+    size = np.ones(n, np.int64)
+    for i in range(n - 1, -1, -1):   # children follow their parent in pre-order
+        if ni[i, 2] < 0:
+            size[i] = 1 + size[ni[i, 0]] + size[ni[i, 1]]
+    return nf[:, :6].copy(), np.arange(n) + size, ni[:, 2].copy()
+
+
+def copy_fields(W):
+    """one ordering's (boxes, skip, tri) from its traversal-layout rows"""
+    return W[:, :6].copy(), W[:, 6].view(np.int32).astype(np.int64), W[:, 7].view(np.int32).astype(np.int64)
+
+
+def walk(boxes, skip, tri, start, stop, base, hit):
+    """the kernel's stackless walk: leaves reached, and nodes visited (indices are absolute; row = index - base)"""
+    ti, leaves, visits = start, [], 0
+    while ti < stop:
+        k = ti - base
+        visits += 1
+        h = hit(boxes[k])
+        if h and tri[k] < 0:
+            ti += 1
+        else:
+            if h:
+                leaves.append(int(tri[k]))
+            ti = int(skip[k])
+    return leaves, visits
+
+
+def slab(o, d):
+    inv = np.divide(1.0, d, out=np.full(3, np.inf), where=d != 0)
+    def hit(b):
+        t1 = (b[:3] - o) * inv
+        t2 = (b[3:] - o) * inv
+        lo = np.nanmax(np.minimum(t1, t2))
+        hi = np.nanmin(np.maximum(t1, t2))
+        return hi >= max(lo, 0.0)
+    return hit
+
+
+def check_orders(sc, n_rays, seed):
+    info = sc.info()
+    r, e, NN = info.split_root, info.split_end, info.n_nodes
+    assert r > 0
+    boxes, skip, tri = original(sc)
+    Wall = sc.walk_orders()
+    M = e - r
+    assert Wall.shape == (8, M, 8)
+    ref_rows = np.sort(np.concatenate([boxes[r:e], tri[r:e, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
+    rng = np.random.default_rng(seed)
+    lo, hi = boxes[r, :3].astype(np.float64), boxes[r, 3:].astype(np.float64)
+    for oct_ in range(8):
+        bx, sk, tr = copy_fields(Wall[oct_])
+        # the same nodes (box, triangle), each once
+        rows = np.sort(np.concatenate([bx, tr[:, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
+        assert np.array_equal(rows, ref_rows)
+        # a well-formed pre-order: a leaf's skip is the next row, an internal node's first child is the next
+        # row and its second child's skip equals its own; every pointer stays in [r + 1, e) or reads NN
+        idx = r + np.arange(M)
+        sk_in = np.where(sk == NN, e, sk)
+        assert np.all((sk_in > idx) & (sk_in <= e))
+        leaf = tr >= 0
+        assert np.all(sk_in[leaf] == idx[leaf] + 1)
+        inner = np.where(~leaf)[0]
+        right = sk_in[inner + 1]
+        assert np.all(right < sk_in[inner])
+        assert np.all(sk_in[right - r] == sk_in[inner])
+        assert sk[0] == NN   # the walk ends at n_nodes
+        # everything hit: all M nodes in row order
+        leaves, visits = walk(bx, sk, tr, r, NN, r, lambda b: True)
+        assert visits == M and len(leaves) == int(leaf.sum())
+    # rays through the subtree's box: the ordering of the ray's octant reaches the DFS walk's leaves, with
+    # the same boxes tested
+    for _ in range(n_rays):
+        tgt = lo + (hi - lo) * rng.random(3)
+        o = tgt + rng.normal(size=3) * (hi - lo).max()
+        d = tgt - o
+        d /= np.linalg.norm(d)
+        oct_ = int(d[0] < 0) | int(d[1] < 0) << 1 | int(d[2] < 0) << 2
+        hit = slab(o, d)
+        ref_leaves, ref_visits = walk(boxes, skip, tri, r, e, 0, hit)
+        bx, sk, tr = copy_fields(Wall[oct_])
+        leaves, visits = walk(bx, sk, tr, r, NN, r, hit)
+        assert sorted(leaves) == sorted(ref_leaves) and visits == ref_visits
+
+
+def test_walk_orders_of_the_adversarial_split_scene():
+    sc = SA.A.build_rt(SA.split_scene())
+    check_orders(sc, n_rays=300, seed=1)
+
+
+def test_walk_orders_of_c5():
+    bvh = np.load(SA.A.__file__.replace("test_skip_adversarial.py", "golden/bvh_scene.npz"))
+    sc = rt.Scene.cornell_c5(bvh["raw_bunny"])
+    check_orders(sc, n_rays=40, seed=2)
+
+
+def test_small_scenes_have_no_walk_orders():
+    assert rt.Scene.cornell().walk_orders() is None
