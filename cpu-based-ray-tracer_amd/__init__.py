@@ -60,7 +60,7 @@ class GroupStats(C.Structure):
     _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
 
 
-_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation"}   # may be absent from an older A/B build
+_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders"}   # may be absent from an older A/B build
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 
