@@ -117,3 +117,36 @@ def test_split_adversarial_matches_oracle(far, env, monkeypatch):
     same = np.mean(np.all(A.bits(acc) == A.bits(oacc), axis=-1))
     assert np.array_equal(A.bits(acc), A.bits(oacc)), f"{same:.4%} of pixels bitwise equal"
     assert np.array_equal(rgba, orgba)
+
+
+@pytest.mark.gpu
+def test_scene_beyond_the_prepass_limit_takes_the_bvh_variant():
+    """A scene of 2^19 triangles and more (the camera pre-pass records carry the triangle in 19 bits) still
+    runs the vertex kernel's BVH variant, without the pre-pass (no megakernel fallback below
+    2^31), bitwise against the oracle: the block of the adversarial split scene tessellated into 526,338
+    triangles (a 513 x 513 grid on each of two faces) inside scene A"""
+    def grid_fast(p0, du, dv, n):   # grid_face's triangles, vectorized
+        i, j = [g.reshape(-1, 1) for g in np.meshgrid(np.arange(n), np.arange(n), indexing="ij")]
+        P = lambda a, b: p0 + du * (a / n) + dv * (b / n)
+        a, b, c, d = P(i, j), P(i + 1, j), P(i + 1, j + 1), P(i, j + 1)
+        return np.stack([np.concatenate([a, b, c], 1), np.concatenate([c, d, a], 1)], 1).reshape(-1, 9).astype(np.float32)
+    g0 = grid_fast(np.array([360.0, 0.0, 280.0]), np.array([100.0, 0.0, 0.0]), np.array([0.0, 150.0, 0.0]), 513)
+    grid = np.concatenate([g0[: 263169], grid_fast(np.array([360.0, 150.0, 280.0]), np.array([100.0, 0.0, 0.0]), np.array([0.0, 0.0, 120.0]), 513)[: 263169]])
+    base = A.scene_a()
+    meshes = base[:-1] + [("grid", grid, A.WHITE, A.NOEM)] + base[-1:]
+    sc = A.build_rt(meshes)
+    assert sc.info().n_tris >= (1 << 19)
+    W, H, spp, seed = 48, 36, 4, 3
+    c = rt.Context(0)
+    try:
+        c.upload(sc)
+        c.resize(W, H)
+        cam, _, _ = rt.camera_default(W, H)
+        rgba, acc = c.render(cam, spp, seed=seed)
+        st = c.stats()
+        assert st.kernel == 3 and st.last_prepass_ms == 0.0
+    finally:
+        c.close()
+    oacc, orgba, _ = O.Scene(meshes).render(W, H, spp, seed=seed)
+    assert np.array_equal(A.bits(acc), A.bits(oacc))
+    assert np.array_equal(rgba, orgba)
