@@ -11,6 +11,7 @@
 #   c5full                 C5 at its full 4096 spp (warm-up at 4096 spp)                            -> c5_4096.jsonl
 #   prof                   rocprofv3 trace + PMC passes of the bench command      -> profiles via profiles/run_rocprof.sh
 #   profc5                 the same for C5 at 64 spp                              -> tools/prof_c5.sh
+#   profc5:K=V             the C5 profile with one knob set (e.g. RT_WALK_ORDER=0)
 #   ab:ARGS                tools/ab_libs.py ARGS (comma-separated, e.g. ab:librt_hip.so,librt_hip_x.so,--spp,256)
 #   sweep:ARGS             tools/sweep_env.py ARGS (comma-separated)
 #   sections:LIB:SCENE:SPP[:W:H] wave cycles per kernel section of an RT_SECTIONS build (tools/prof_one.py)
@@ -53,6 +54,10 @@ for step in "$@"; do
       bash profiles/run_rocprof.sh "$TAG" ;;
     profc5)
       bash tools/prof_c5.sh "${TAG}_c5" 64 ;;
+    profc5:*)
+      # the same under one knob (K=V), e.g. profc5:RT_WALK_ORDER=0 -> gpurun_out/prof_TAG_c5_RT_WALK_ORDER0
+      kv=${step#profc5:}
+      env "$kv" bash tools/prof_c5.sh "${TAG}_c5_${kv//=/}" 64 ;;
     ab:*)
       IFS=',' read -r -a a <<< "${step#ab:}"
       timeout -k 10 400 python3 -u tools/ab_libs.py "${a[@]}" > "$OUT/ab_$n.json" 2>&1 || { tail -20 "$OUT/ab_$n.json"; exit 1; }
