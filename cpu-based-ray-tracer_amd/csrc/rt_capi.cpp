@@ -44,7 +44,6 @@ struct rt_ctx {
     // entry plus a 4-byte material that misses L2 on its own line: C4 221 -> 133 B/sample of L2 -> fabric
     // traffic): RT_RING_PACK 0 off, 1 BVH variant only, 2 both variants
     uint32_t ring_pack = 2;
-    bool bvh_small_lds = true;   // RT_BVH_SMALL_LDS=0: the BVH variant reads materials and light tables from HBM
     bool bvh_prepass = true;     // split scenes: the BVH variant's paths start from the camera pre-pass (RT_BVH_PREPASS=0: off)
     bool pre_defer_walk = true;  // ... whose camera rays into the walked subtree are traced by the path kernel (RT_PRE_DEFER=0: walked there)
     float4 *d_wmats = nullptr, *d_plights = nullptr, *d_went = nullptr, *d_wtris = nullptr;
@@ -128,6 +127,9 @@ struct rt_ctx {
 namespace {
 
 constexpr size_t kMaxLdsScene = 48 * 1024;   // scenes up to ~700 triangles live in LDS
+// the vertex kernel's BVH variant: materials + light tables + split slots in LDS beside its 17 KB of lane
+// state (~2500 light triangles; C5: 1.9 KB)
+constexpr size_t kMaxBvhSmallLds = 40 * 1024;
 constexpr uint32_t kStackDepth = 192;   // EXACT fold stack; RR 0.8 => P(depth > 192) ~ 2.5e-19 per sample
 constexpr uint32_t kStackDepthMax = 2048;
 constexpr uint32_t kResampleDepth = 4096;   // the kernels' path-length cap (P = rr^4096)
@@ -439,7 +441,6 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (const char* e = rt_knob("RT_BVH_SMALL_LDS")) c->bvh_small_lds = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_BVH_PREPASS")) c->bvh_prepass = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_PRE_DEFER")) c->pre_defer_walk = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LDS_PAD")) c->lds_pad = (uint32_t)std::strtoul(e, nullptr, 10);
@@ -764,8 +765,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const bool coh_box = c->vertex && P.n_lboxes > 0 && lds && !count && !c->gb_next && !whitted && P.n_mats < (1u << 14);
     // (the camera pre-pass's records carry a triangle index in 19 bits, rt_kernels.h crec: only the leaf-box
     // variant runs the pre-pass, and its scenes have <= 64 triangles; the BVH variant carries full indices)
+    // (the BVH variant stages the materials and light tables in LDS with its lane state: a scene whose tables
+    // exceed kMaxBvhSmallLds renders on the megakernel)
+    const size_t bvh_small_bytes = (size_t)(2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris + 3 * P.n_split_leaves) * sizeof(float4);
     const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31) &&
-                         P.n_mats < (1u << 14);
+                         P.n_mats < (1u << 14) && bvh_small_bytes <= kMaxBvhSmallLds;
     const bool coh = coh_box || coh_bvh;
     // the camera pre-pass: the leaf-box variant always; the BVH variant for a split scene, whose camera rays are
     // traced like the path kernel's split phase (records carry the triangle in 19 bits, rt_kernels.h crec)
@@ -778,12 +782,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (coh_box) {   // the vertex kernel reads the leaf boxes with scalar loads and the nodes from HBM: neither is staged
         P.lds_scene_quads -= 2 * P.n_lboxes + 2 * P.n_nodes;
     }
-    if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; materials and the light
-        // tables stay in LDS when they are small (C5: 21 quads)
-        const uint32_t small = 2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris;
-        P.lds_small = (c->bvh_small_lds && small <= 64u) ? 1u : 0u;
-        // the split's outside triangles (<= 32 x 3 quads) are staged after them, always
-        P.lds_scene_quads = (P.lds_small ? small : 0u) + 3u * P.n_split_leaves;
+    if (coh_bvh) {   // the BVH variant reads the nodes and triangles from HBM; the materials and the light
+        // tables are in LDS (C5: 21 quads), the split's outside triangles (<= 32 x 3 quads) after them
+        P.lds_scene_quads = (uint32_t)(bvh_small_bytes / sizeof(float4));
         P.ring_pack = (c->ring_pack >= 1 && c->hdr.n_mats <= 8) ? 1u : 0u;
         P.thresh = P.split_root != 0u ? c->sthresh : c->vthresh;
         P.steps = P.split_root != 0u ? c->ssteps : c->vsteps;

@@ -276,9 +276,11 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
     if (BVH) {
         S.nodes = P.nodes; S.tris = P.tris; S.mats = P.mats; S.lnodes = P.lnodes; S.ltris = P.ltris; S.lboxes = nullptr;
         uint32_t at = 0;
-        if (P.lds_small != 0u) {
-            // the small tables in LDS (mats | lnodes | ltris): the service's material and the light
-            // sample then wait on no HBM load
+        {
+            // the small tables in LDS (mats | lnodes | ltris; the host runs this variant only when they fit):
+            // the service's material and the light sample wait on no HBM load, and every access to them is
+            // an LDS read with a 32-bit address (a table that could be in LDS or HBM is a generic pointer:
+            // flat loads and 64-bit addresses in VGPRs)
             const uint32_t mq = 2 * P.n_mats, lq = P.n_lnodes, ltq = 4 * P.n_ltris;
             float4* dm = lds_scene;
             float4* dl = dm + mq;
@@ -1183,7 +1185,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         cm &= cm - 1;
                         const bool useA = bit < 32u;
                         // the slot's triangle, staged in LDS after the small tables (a, e1, (e2, bits(triangle)))
-                        const float4* T = lds_scene + (kargs4().lds_small ? 2u * kargs4().n_mats + kargs4().n_lnodes + 4u * kargs4().n_ltris : 0u) + 3u * (bit & 31u);
+                        const float4* T = lds_scene + (2u * kargs4().n_mats + kargs4().n_lnodes + 4u * kargs4().n_ltris) + 3u * (bit & 31u);
                         const float4 t0 = T[0], t1 = T[1], t2 = T[2];
                         const int tri = f2i(t2.w);
                         double t;

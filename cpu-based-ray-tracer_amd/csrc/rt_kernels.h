@@ -21,8 +21,8 @@ struct KParams {
     // the subtree's near-first orderings (rt_scene.h FlatScene::wcopies; null: off): ordering o's node k at
     // wcopies[2 * k + o * wcopy_stride], k in [split_root, split_end) (the pointer is offset by -2 * split_root)
     const float4* wcopies; uint32_t wcopy_stride;
-    uint32_t lds_small;   // the BVH variant: the small tables (mats | lnodes | ltris) are staged in LDS; the split's
-                          // outside triangles (3 float4 per slot: a, e1, (e2, bits(triangle))) follow them
+    // (the BVH variant stages the small tables (mats | lnodes | ltris) in LDS, the split's outside triangles
+    //  (3 float4 per slot: a, e1, (e2, bits(triangle))) after them; rt_capi.cpp checks that they fit)
     // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex
     // kernel's BVH variant walks it for waves whose rays all have a finite reciprocal direction
     const uint4* qnodes; const float4* tabc; const float4* tnrm; uint32_t use_qnodes;

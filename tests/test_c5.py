@@ -161,7 +161,7 @@ def test_full_frame_digest(ctx, fixture):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"},
-                                 {"RT_BVH_SMALL_LDS": "0"}, {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_THRESH": "0", "RT_STEPS": "1"},
+                                 {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_THRESH": "0", "RT_STEPS": "1"},
                                  {"RT_THRESH": "64"}, {"RT_BVH_PREPASS": "0"}, {"RT_BVH_PREPASS": "0", "RT_FORCE_WALK": "1"},
                                  {"RT_PRE_DEFER": "0"}, {"RT_WALK_ORDER": "0"}, {"RT_WALK_ORDER": "0", "RT_BVH_PREPASS": "0"}])
 def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):

@@ -150,3 +150,28 @@ def test_scene_beyond_the_prepass_limit_takes_the_bvh_variant():
     oacc, orgba, _ = O.Scene(meshes).render(W, H, spp, seed=seed)
     assert np.array_equal(A.bits(acc), A.bits(oacc))
     assert np.array_equal(rgba, orgba)
+
+
+@pytest.mark.gpu
+def test_light_tables_beyond_lds_take_the_megakernel():
+    """The BVH variant keeps the materials and light tables in LDS (rt_capi.cpp kMaxBvhSmallLds): a scene whose
+    light is a 3200-triangle mesh (its tables ~200 KB) renders on the megakernel instead, bitwise against the
+    oracle"""
+    base = A.scene_a()
+    light = grid_face(np.array([213.0, A.LY, 227.0]), np.array([130.0, 0.0, 0.0]), np.array([0.0, 0.0, 105.0]), 40)
+    meshes = base[:-1] + [("light", light, base[-1][2], base[-1][3])]
+    W, H, spp, seed = 48, 36, 4, 9
+    sc = A.build_rt(meshes)
+    assert sc.info().n_light_tris == 3200
+    c = rt.Context(0)
+    try:
+        c.upload(sc)
+        c.resize(W, H)
+        cam, _, _ = rt.camera_default(W, H)
+        rgba, acc = c.render(cam, spp, seed=seed)
+        assert c.stats().kernel == 0   # RT_KERNEL_MEGA
+    finally:
+        c.close()
+    oacc, orgba, _ = O.Scene(meshes).render(W, H, spp, seed=seed)
+    assert np.array_equal(A.bits(acc), A.bits(oacc))
+    assert np.array_equal(rgba, orgba)
