@@ -1259,7 +1259,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         // in the near-first ordering of its direction's octant when the scene has them
                         const float4* wn = S.nodes;
                         if (Q.wcopies != nullptr && (decltype(kind)::value || finite3(r.rcp)))
-                            wn = Q.wcopies + ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) * Q.wcopy_stride;
+                            wn = Q.wcopies + (((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) & Q.wcopy_mask) * Q.wcopy_stride;
                         for (uint32_t s = 0; s < steps && ti < NN; ++s) {
                             const float4 q0 = wn[2 * ti];
                             const float4 q1 = wn[2 * ti + 1];
