@@ -739,6 +739,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     }
     P.band = c->band; P.rank = c->rank; P.nranks = c->nranks; P.n_local_rows = c->local_rows;
     P.tiles_x = (c->W + 7) / 8;
+    P.r_band = (float)(1.0 / (double)std::max<uint32_t>(1u, P.band));
+    P.r_tiles_x = (float)(1.0 / (double)std::max<uint32_t>(1u, P.tiles_x));
     const uint64_t items = (uint64_t)((c->local_rows + 7) / 8) * P.tiles_x * 64;
     if (items >= 0xFFFFFFFFull) { c->err = "image too large for one launch"; return RT_ERR_INVALID; }
     P.n_items = (uint32_t)items;
@@ -927,6 +929,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);
                     if (nseg >= (1ull << (32 - Q.seg_shift))) { c->err = "too many samples for one pass"; return RT_ERR_INVALID; }
                     Q.n_segments = (uint32_t)nseg;
+                    Q.r_n_tiles = (float)(1.0 / (double)std::max<uint32_t>(1u, Q.n_tiles));
+                    // the path kernel's record decode divides segment, tile and local row by uniform divisors
+                    Q.div24 = (nseg < (1u << 24) && Q.n_tiles < (1u << 24) && c->local_rows < (1u << 24) && Q.band < (1u << 24) &&
+                               Q.tiles_x < (1u << 24)) ? 1u : 0u;
                     if ((nseg << Q.seg_shift) > c->crec_quads) {
                         HIPC(c, hipStreamSynchronize(c->stream));
                         dfree(c->d_crec);

@@ -343,6 +343,9 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
     // (vmcnt counts both), and a path-tracing iteration that read the accumulator after its parked
     // samples and fold-level stores waited for their write-back.
     auto complete = [&](V3 L, uint32_t local, uint32_t fidx) { park_sample(kargs4(), L, local, fidx); };
+    // x mod R for x in [0, 2R): every ring-distance expression below is a position (< R) plus R minus a
+    // position or a level count in [1, R), so one conditional subtract replaces the generic 32-bit remainder
+    auto ring_wrap = [](uint32_t x, uint32_t R) { return x >= R ? x - R : x; };
     // up to N fold steps of the draining path, L = Ld_k + ((((L * brdf_k) * cos_k) / PDF) / RR)
     // (MC/Renderer.cpp:208,213), inner level first, from ring position `pos` down; the N ring loads are
     // issued together (levels past the fold re-read the first one, unused).  Returns the levels folded.
@@ -673,12 +676,12 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     // their slot)
                     bool fits = lvl < R;
                     if (fits && dleft != 0u) {
-                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
-                        fits = (pos + R - lo) % R >= dleft;
+                        const uint32_t lo = ring_wrap(lsu(VS_DPOS) + R + 1u - dleft, R);
+                        fits = ring_wrap(pos + R - lo, R) >= dleft;
                     } else if (PEND && fits && hasPend) {
                         const uint32_t pd = lsu(VS_PEND), pm = pd >> 12;
-                        const uint32_t lo = ((pd & 0xFFFu) + R + 1u - pm) % R;
-                        fits = (pos + R - lo) % R >= pm + 1u;
+                        const uint32_t lo = ring_wrap((pd & 0xFFFu) + R + 1u - pm, R);
+                        fits = ring_wrap(pos + R - lo, R) >= pm + 1u;
                     }
                     if (fits) {
                         if (Q.ring_pack) {
@@ -742,8 +745,8 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         if (top >= R) top -= R;
                         uint32_t mp = top + 1u;
                         if (mp >= R) mp -= R;
-                        const uint32_t lo = (lsu(VS_DPOS) + R + 1u - dleft) % R;
-                        if (m + 1u < R && (mp + R - lo) % R >= dleft) {
+                        const uint32_t lo = ring_wrap(lsu(VS_DPOS) + R + 1u - dleft, R);
+                        if (m + 1u < R && ring_wrap(mp + R - lo, R) >= dleft) {
                             Q.stack_ld[RING_AT(mp)] = make_float4(L.x, L.y, L.z, __uint_as_float(fidx));
                             lsu(VS_PEND) = top | (m << 12);
                             lsu(VS_PLOC) = local;
@@ -790,12 +793,12 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             CKParams& Q = kargs4();
             const uint32_t tag = __float_as_uint(rec.w);
             const uint32_t sg = rid >> Q.seg_shift;
-            const uint32_t c = sg / Q.n_tiles, tile = sg - c * Q.n_tiles;
-            const uint32_t trow = tile / Q.tiles_x, tcol = tile - trow * Q.tiles_x;
+            const uint32_t c = udiv_u(sg, Q.n_tiles, Q.r_n_tiles, Q.div24), tile = sg - c * Q.n_tiles;
+            const uint32_t trow = udiv_u(tile, Q.tiles_x, Q.r_tiles_x, Q.div24), tcol = tile - trow * Q.tiles_x;
             const uint32_t pit = (tag >> 19) & 63u;
             const uint32_t lr = trow * 8u + (pit >> 3), lx = tcol * 8u + (pit & 7u);
             // local row -> global row (row bands dealt round-robin over ranks)
-            const uint32_t band_k = lr / Q.band, in_band = lr - band_k * Q.band;
+            const uint32_t band_k = udiv_u(lr, Q.band, Q.r_band, Q.div24), in_band = lr - band_k * Q.band;
             const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
             const uint32_t pix = y * Q.W + lx;
             const uint32_t frame = Q.first_frame + c * Q.seg_frames + ((tag >> 25) & 63u);

@@ -88,6 +88,23 @@ __device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a
 
 __device__ __forceinline__ int f2i(float f) { return __float_as_int(f); }
 
+// x / d for x < 2^24 and 1 <= d < 2^24, from rd = (float)(1 / d): (float)x is exact and the float quotient is
+// within one of x / d (relative error <= 2^-23, exact for d a power of two), so one correction either way
+// makes it exact -- full-rate instructions, where the generic 32-bit division is ~22 with five at quarter rate
+__device__ __forceinline__ uint32_t udiv24(uint32_t x, uint32_t d, float rd)
+{
+    uint32_t q = (uint32_t)((float)x * rd);
+    const int32_t r = (int32_t)(x - __umul24(q, d));
+    if (r < 0) --q;
+    else if (r >= (int32_t)d) ++q;
+    return q;
+}
+// the launch's uniform choice: udiv24 when every dividend is below 2^24 (KParams::div24), else x / d
+__device__ __forceinline__ uint32_t udiv_u(uint32_t x, uint32_t d, float rd, uint32_t fast)
+{
+    return fast ? udiv24(x, d, rd) : x / d;
+}
+
 constexpr float PI_F = 3.141592653589793f;            // MC/WhittedUtilities.h:20
 constexpr float INTERSECTION_CORRECTION = 0.00001f;   // MC/WhittedUtilities.h:18
 

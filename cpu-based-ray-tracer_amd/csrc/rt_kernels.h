@@ -44,6 +44,9 @@ struct KParams {
     // pixels of this device: row bands of `band` rows dealt round-robin over `nranks`
     uint32_t band, rank, nranks, n_local_rows;
     uint32_t tiles_x; uint32_t n_items;
+    // (float)(1 / d) of the uniform divisors band, tiles_x, n_tiles (rt_device.h udiv24), and whether every
+    // dividend of this launch is below 2^24 (else the generic division)
+    float r_band, r_tiles_x, r_n_tiles; uint32_t div24;
     // frame chunks: a pixel's n_frames are split into n_chunks work items of chunk_frames frames so
     // that a frame-range tail does not serialize a launch with few pixels per lane (multi-GPU bands);
     // chunk 0 accumulates into accum, later chunks store their samples (3 planes of floats,
