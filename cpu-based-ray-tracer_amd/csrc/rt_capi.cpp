@@ -931,8 +931,11 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.n_segments = (uint32_t)nseg;
                     Q.r_n_tiles = (float)(1.0 / (double)std::max<uint32_t>(1u, Q.n_tiles));
                     // the path kernel's record decode divides segment, tile and local row by uniform divisors
+                    // (and multiplies: every factor < 2^24 -- the image's W and H too -- and every product, a pixel
+                    // index at most, < 2^32)
                     Q.div24 = (nseg < (1u << 24) && Q.n_tiles < (1u << 24) && c->local_rows < (1u << 24) && Q.band < (1u << 24) &&
-                               Q.tiles_x < (1u << 24)) ? 1u : 0u;
+                               Q.tiles_x < (1u << 24) && c->W < (1u << 24) && c->H < (1u << 24) && Q.nranks < (1u << 24) &&
+                               (uint64_t)c->W * c->H < (1ull << 32) && Q.n_frames < (1u << 24)) ? 1u : 0u;
                     if ((nseg << Q.seg_shift) > c->crec_quads) {
                         HIPC(c, hipStreamSynchronize(c->stream));
                         dfree(c->d_crec);

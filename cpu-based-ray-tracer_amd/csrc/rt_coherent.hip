@@ -255,7 +255,9 @@ constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
 // fold ring layout: lane-major ([thread][position]): a lane's consecutive levels share cache lines, so a
 // drain read follows its push in L2
 // (a 32-bit index: lanes x depth < 2^32, checked on the host; one register for the lane's base, no 64-bit product)
-#define RING_AT(p) ((uint32_t)(gtid * Q.stack_depth + (p)))
+// (gtid < 2^20 and the ring < 2^12 positions: the 24-bit multiply is exact and full rate, rt_capi.cpp keeps the
+// ring's total size below 2^32)
+#define RING_AT(p) ((uint32_t)(__umul24(gtid, Q.stack_depth) + (p)))
 
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
@@ -793,16 +795,17 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             CKParams& Q = kargs4();
             const uint32_t tag = __float_as_uint(rec.w);
             const uint32_t sg = rid >> Q.seg_shift;
-            const uint32_t c = udiv_u(sg, Q.n_tiles, Q.r_n_tiles, Q.div24), tile = sg - c * Q.n_tiles;
-            const uint32_t trow = udiv_u(tile, Q.tiles_x, Q.r_tiles_x, Q.div24), tcol = tile - trow * Q.tiles_x;
+            // (with div24 every factor below is < 2^24 and every product < 2^32: 24-bit multiplies, full rate)
+            const uint32_t c = udiv_u(sg, Q.n_tiles, Q.r_n_tiles, Q.div24), tile = sg - mul_u(c, Q.n_tiles, Q.div24);
+            const uint32_t trow = udiv_u(tile, Q.tiles_x, Q.r_tiles_x, Q.div24), tcol = tile - mul_u(trow, Q.tiles_x, Q.div24);
             const uint32_t pit = (tag >> 19) & 63u;
             const uint32_t lr = trow * 8u + (pit >> 3), lx = tcol * 8u + (pit & 7u);
             // local row -> global row (row bands dealt round-robin over ranks)
-            const uint32_t band_k = udiv_u(lr, Q.band, Q.r_band, Q.div24), in_band = lr - band_k * Q.band;
-            const uint32_t y = (Q.rank + band_k * Q.nranks) * Q.band + in_band;
-            const uint32_t pix = y * Q.W + lx;
-            const uint32_t frame = Q.first_frame + c * Q.seg_frames + ((tag >> 25) & 63u);
-            lsu(VS_LOCAL) = lr * Q.W + lx;
+            const uint32_t band_k = udiv_u(lr, Q.band, Q.r_band, Q.div24), in_band = lr - mul_u(band_k, Q.band, Q.div24);
+            const uint32_t y = mul_u(Q.rank + mul_u(band_k, Q.nranks, Q.div24), Q.band, Q.div24) + in_band;
+            const uint32_t pix = mul_u(y, Q.W, Q.div24) + lx;
+            const uint32_t frame = Q.first_frame + mul_u(c, Q.seg_frames, Q.div24) + ((tag >> 25) & 63u);
+            lsu(VS_LOCAL) = mul_u(lr, Q.W, Q.div24) + lx;
             lsu(VS_PIX) = pix;
             lsu(VS_FRAME) = frame;
             g.start(pix, frame, !Q.has_light);   // the vertex draws continue after the 2 camera draws

@@ -99,6 +99,11 @@ __device__ __forceinline__ uint32_t udiv24(uint32_t x, uint32_t d, float rd)
     else if (r >= (int32_t)d) ++q;
     return q;
 }
+// a * b, as a 24-bit multiply when the launch's factors are below 2^24 and its products below 2^32 (fast)
+__device__ __forceinline__ uint32_t mul_u(uint32_t a, uint32_t b, uint32_t fast)
+{
+    return fast ? __umul24(a, b) : a * b;
+}
 // the launch's uniform choice: udiv24 when every dividend is below 2^24 (KParams::div24), else x / d
 __device__ __forceinline__ uint32_t udiv_u(uint32_t x, uint32_t d, float rd, uint32_t fast)
 {
