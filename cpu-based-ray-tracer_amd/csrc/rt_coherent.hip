@@ -210,6 +210,9 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_COH_BVH_MIN_WAVES
 #define RT_COH_BVH_MIN_WAVES 8
 #endif
+#ifndef RT_BVH_DIV_FAST   // the BVH variant's divisions: IEEE sequences (0) or rt_device.h div_fast (1, A/B)
+#define RT_BVH_DIV_FAST 0
+#endif
 #ifndef RT_COH_BVH_PRE_MIN_WAVES
 #define RT_COH_BVH_PRE_MIN_WAVES 7
 #endif
@@ -336,8 +339,9 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
     // the leaf-box variant divides with rt_device.h div_fast (y = the divisor's correctly rounded
     // reciprocal; C4 +1.1 %); the BVH variant keeps the IEEE division sequence (its register budget: C5
     // -2.5 % with div_fast)
-    auto sdiv = [](float x, float d, float y) { return BVH ? x / d : div_fast(x, d, y); };
-    auto vdiv = [](V3 a, float d, float y) { return BVH ? divs(a, d) : divs_fast(a, d, y); };
+    constexpr bool IEEE_DIV = BVH && !RT_BVH_DIV_FAST;
+    auto sdiv = [](float x, float d, float y) { return IEEE_DIV ? x / d : div_fast(x, d, y); };
+    auto vdiv = [](V3 a, float d, float y) { return IEEE_DIV ? divs(a, d) : divs_fast(a, d, y); };
     // a finished sample is parked in the frame-major sample buffer (4-frame blocks: the 4 frames of a
     // block of one pixel are 48 contiguous bytes); finalize_chunks_kernel then accumulates every
     // pixel's samples in frame order (MC/Renderer.cpp:128-133).  The kernel issues no global load
@@ -870,7 +874,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     const float4 mb = S.mats[2 * mat];
                     const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
                     const V3 ldu = vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
-                                             BVH ? 0.0f : rcp_f32(sd2)),
+                                             IEEE_DIV ? 0.0f : rcp_f32(sd2)),
                                         Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
                     st3(VS_LD, ldu);
                     dB = wl;
@@ -925,7 +929,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             cy = cy * 2.0f - 1.0f;
             float tg[4];
             mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], BVH ? 0.0f : rcp_f32(tg[3])));
+            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], IEEE_DIV ? 0.0f : rcp_f32(tg[3])));
             float wd[4];
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};

@@ -52,6 +52,9 @@ __device__ __forceinline__ float rcp_f32(float x)
     return 1.0f / x;
 }
 
+#ifndef RT_DIV_ZERO_FAST
+#define RT_DIV_ZERO_FAST 1
+#endif
 // x / d correctly rounded, from y = RN(1/d): q = RN(x * y), the exact residual r = x - q * d (one fma),
 // then RN(q + r * y) -- Markstein's correction.  Checked bit for bit against the IEEE division for every
 // x with 2^-100 <= |x| < 2^100 and a list of divisors (tools/verify_div.hip); div_fast takes the IEEE
@@ -65,7 +68,15 @@ __device__ __forceinline__ float div_fast_core(float x, float d, float y)
 __device__ __forceinline__ float div_fast(float x, float d, float y)
 {
     const float ax = __builtin_fabsf(x), ad = __builtin_fabsf(d);
-    if (ax >= 0x1p-100f && ax < 0x1p100f && ad >= 0x1p-20f && ad < 0x1p20f) return div_fast_core(x, d, y);
+    if (ad >= 0x1p-20f && ad < 0x1p20f) {
+        if (ax >= 0x1p-100f && ax < 0x1p100f) return div_fast_core(x, d, y);
+#if RT_DIV_ZERO_FAST
+        // a zero numerator (an occluded or back-facing direct term, a black path's fold) is common: +-0 / d is
+        // +-0 with the sign of x times the sign of d, which x * y gives exactly (y = RN(1 / d) has d's sign);
+        // without this a wave with one zero lane ran the IEEE division sequence too
+        if (x == 0.0f) return x * y;
+#endif
+    }
     return x / d;
 }
 
