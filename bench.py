@@ -124,6 +124,31 @@ def host_cpu():
             "omp_num_threads": omp or None, "cpu0_smt_siblings": smt}
 
 
+def smt_pairs(affinity, n):
+    """Up to n physical cores (sysfs thread_siblings_list) with both SMT siblings in `affinity`."""
+    out, seen = [], set()
+    for c in sorted(affinity):
+        if c in seen:
+            continue
+        try:
+            txt = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            continue
+        sib = []
+        for part in txt.split(","):
+            if "-" in part:
+                a, b = part.split("-")
+                sib.extend(range(int(a), int(b) + 1))
+            elif part.strip():
+                sib.append(int(part))
+        seen.update(sib)
+        if len(sib) >= 2 and all(x in affinity for x in sib[:2]):
+            out.append((sib[0], sib[1]))
+        if len(out) >= n:
+            break
+    return out
+
+
 def cpu_baseline(W, H, seconds):
     """The reference renderer timed on this host's cores (SURVEY.md section 8(d) "CPU baseline").
 
@@ -165,18 +190,36 @@ def cpu_baseline(W, H, seconds):
         rate = n / dt / 1e6
         per_thread = rate / threads
         est = per_thread * cpu["physical_cores_per_socket"]
-        # what SMT adds to a core (the estimate above runs one thread per physical core): one thread on a
-        # core against two on its SMT siblings, ~2 s each, when the affinity mask holds a sibling pair
+        # what SMT adds to a core (the estimate above runs one thread per physical core), measured on up to 8
+        # physical cores whose two SMT siblings are both in this job's CPUs (inside the 16-CPU quota): the same
+        # cores with one thread each, then with two (one per sibling), >= 5 s each, 3 alternating repeats; the
+        # median gain and its spread (a 2-second one-core probe moved the ratio by +-7 %)
         smt = None
-        sib = [int(c) for c in (cpu["cpu0_smt_siblings"] or "").replace("-", ",").split(",") if c.strip().isdigit()]
-        aff = os.sched_getaffinity(0)
-        if len(sib) >= 2 and sib[0] in aff and sib[1] in aff:
-            spp1 = max(1, int(2.0 * per_thread * 1e6 / (W * H)))
-            na, ta = run(spp1, 1, [sib[0]])
-            nb, tb = run(2 * spp1, 2, sib[:2])
-            gain = (nb / tb) / (na / ta)
-            smt = {"cpus": sib[:2], "gain": round(gain, 3), "value": round(est * gain, 2),
-                   "how": "the one-thread-per-core estimate x the throughput two SMT siblings add over one thread on their core"}
+        pairs = smt_pairs(os.sched_getaffinity(0), max(1, min(8, threads // 2)))
+        if pairs:
+            one = [p[0] for p in pairs]
+            both = [c for p in pairs for c in p]
+            spp1 = max(1, int(5.0 * per_thread * len(one) * 1e6 / (W * H)))
+            r1, r2 = [], []
+            for _ in range(3):
+                na, ta = run(spp1, len(one), one)
+                r1.append(na / ta / 1e6)
+                nb, tb = run(spp1 * 2, len(both), both)   # ~2x the rate if SMT doubled it: keep >= 5 s
+                r2.append(nb / tb / 1e6)
+            gains = sorted(b / a for a, b in zip(r1, r2))
+            gain = gains[1]
+            per_core_1 = float(np.median(r1)) / len(one)
+            per_core_2 = float(np.median(r2)) / len(one)
+            smt = {"cores": len(pairs), "cpus_one_per_core": one, "cpus_both_siblings": both,
+                   "gain": round(gain, 4), "gain_min": round(gains[0], 4), "gain_max": round(gains[-1], 4),
+                   "value": round(est * gain, 2),
+                   "value_min": round(est * gains[0], 2), "value_max": round(est * gains[-1], 2),
+                   "pinned_per_core_msamples": {"one_thread": round(per_core_1, 4), "two_siblings": round(per_core_2, 4)},
+                   "pinned_socket_estimate": round(per_core_2 * cpu["physical_cores_per_socket"], 2),
+                   "runs": {"one_thread_msamples": [round(x, 3) for x in r1], "two_siblings_msamples": [round(x, 3) for x in r2],
+                            "seconds_each": ">= 5", "spp_one": spp1},
+                   "how": f"the one-thread-per-core estimate x the median (of 3) throughput gain of {len(pairs)} physical cores "
+                          f"running two threads (both SMT siblings) over the same cores running one"}
         return {"value": round(rate, 3), "unit": "Msamples/s", "cores": threads, "kind": "reference",
                 "rng": "shipped (thread_local mt19937 seed 5489, MSVC 32-bit distribution, persistent pool)",
                 "cpu_model": cpu["model"], "sockets": cpu["sockets"],
@@ -193,7 +236,7 @@ def cpu_baseline(W, H, seconds):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo):
+def frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo, use_dist):
     """The metric's second half ("per-pixel RMSE vs CPU ref", BASELINE.json) for the LAST timed frame, after
     the timed region.  tests/golden/full_c4.npz (and full_c2.npz) hold the reference's frame at the
     benchmarked configuration's full spp (frames 1..spp, seed 0, RR 0.8; the accumulation of
@@ -221,7 +264,7 @@ def frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo):
     cb = np.clip(b / np.float32(spp), 0.0, 1.0).astype(np.float64)
     sums = np.array([float(((ca - cb) ** 2).sum()), float(np.all(a.view(np.uint32) == b.view(np.uint32), axis=-1).sum()),
                      float(a.shape[0] * a.shape[1]), float(np.abs(ca - cb).max(initial=0.0))], np.float64)
-    if world > 1:
+    if use_dist:
         t = torch.tensor(sums[:3], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
         dist.all_reduce(t)
         m = torch.tensor(sums[3:], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
@@ -255,6 +298,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: RCCL on device tensors (the product path) or gloo on host-staged bands (tests: "
                          "several ranks on one GPU, where RCCL needs one GPU per rank)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the N > 1 path's collectives even with one rank: init_process_group, the all-gather of "
+                         "the bands and the MAX all-reduce of the time (exercises RCCL on a one-GPU box)")
     ap.add_argument("--dump-image", default=None, help="rank 0 saves the gathered RGBA8 frame (.npy, row 0 = bottom)")
     args = ap.parse_args()
 
@@ -264,9 +310,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    gloo = world > 1 and args.dist_backend == "gloo"
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    gloo = use_dist and args.dist_backend == "gloo"
+    if use_dist:
         # one GPU per rank (RCCL); with gloo several ranks may share a GPU
+        if world == 1 and "MASTER_ADDR" not in os.environ:   # --force-dist without a launcher
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
         torch.cuda.set_device(local % torch.cuda.device_count() if gloo else local)
         dist.init_process_group(args.dist_backend)
     else:
@@ -287,7 +340,7 @@ def main():
     cam, _, _ = rt.camera_default(W, H)
 
     rtdist = load_dist()
-    gat = rtdist.ImageGather(W, H, args.band, rank, world, torch.device("cpu") if gloo else dev)
+    gat = rtdist.ImageGather(W, H, args.band, rank, world, torch.device("cpu") if gloo else dev, collective=use_dist)
     stage = torch.zeros(gat.max_rows * W, dtype=torch.int32, device=dev) if gloo else None
     assert gat.n_local == ctx.local_rows
     kernel_ms, main_ms, pre_ms = [], [], []
@@ -311,17 +364,17 @@ def main():
         step()
     kernel_ms.clear(); main_ms.clear(); pre_ms.clear()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     per_rank = [elapsed]
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
         parts = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(parts, t)
@@ -333,7 +386,7 @@ def main():
     if args.dump_image and rank == 0:
         np.save(args.dump_image, gat.image.cpu().numpy().view(np.uint32).reshape(H, W))
     # the metric's second half: the last timed frame against the reference (outside the timed region)
-    parity = frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo)
+    parity = frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo, use_dist)
 
     # Roofline of the path's kernels on this rank.  SURVEY.md 8(d): there is no dense contraction and the
     # Cornell scene lives on chip, so the binding roof for C2/C4 is the vector ALU; the sample is priced by
@@ -368,9 +421,15 @@ def main():
         # a rocprofv3 counter pass of this build and shape (profiles/): HBM bytes per launch and the
         # kernels' VALU issue fraction / lane utilization
         roof["traffic"] = pmc.get("hbm_bytes_per_launch")
-        # the path kernel's measured L2 -> fabric bytes per launch over its live launch time, against HBM's 8 TB/s
+        # the path kernel's measured L2 -> fabric bytes per launch over its live launch time, against HBM's 8 TB/s:
+        # an UPPER bound of its HBM use (the request-size counters count at the L2's fabric side, Infinity Cache
+        # hits included), so it is named for what it measures
         if roof["traffic"] and main_s > 0:
-            roof["hbm_frac_measured"] = round(roof["traffic"] / main_s / HBM_PEAK_BYTES_PER_S, 4)
+            roof["fabric_frac_of_hbm_peak"] = round(roof["traffic"] / main_s / HBM_PEAK_BYTES_PER_S, 4)
+        if pmc.get("split_rdreq_dram") is not None:
+            # the requests of those that went to DRAM (TCC_EA0_{RD,WR}REQ_DRAM), per sample
+            roof["dram_requests_per_sample"] = {"read": round(pmc["split_rdreq_dram"] / per_launch, 4),
+                                                "write": round((pmc.get("split_wrreq_dram") or 0.0) / per_launch, 4)}
         roof["counters"] = {"file": pmc["_file"], "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
                             "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                             "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample"),
@@ -407,16 +466,18 @@ def main():
             "vs_baseline": None, "dtype": "f32+f64", "data": "synthetic (reference Cornell box scene, Philox RNG seed 0)",
             "config": {"workload": f"C4 cornell {W}x{H} {spp}spp", "width": W, "height": H, "spp": spp, "rr": 0.8,
                        "seed": 0, "band_rows": args.band, "accumulation": "fast" if args.fast else "exact",
-                       "parallelism": f"row-bands x{world}", "dist_backend": args.dist_backend if world > 1 else None},
+                       "parallelism": f"row-bands x{world}", "dist_backend": args.dist_backend if use_dist else None},
             "roofline": roof,
             "parity": parity,
             "fast_mode": fast,
             "rank_elapsed_s": [round(x, 6) for x in per_rank],
+            "collectives": ({"backend": args.dist_backend, "ops": ["all_gather_into_tensor" if not gloo else "all_gather", "all_gather", "all_reduce(MAX)", "barrier"],
+                             "forced_one_rank": world == 1} if use_dist else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -17,7 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 
 # include/rt_capi.h RT_API_VERSION: the struct layouts (rt_stats, rt_scene_info, ...) this binding declares
-API_VERSION = 2
+API_VERSION = 3
 
 RT_OK = 0
 RT_ERR_OVERFLOW = -6
@@ -54,7 +54,7 @@ class Stats(C.Structure):
                 ("cycles_service", C.c_uint64), ("cycles_queue", C.c_uint64), ("cycles_trace", C.c_uint64),
                 ("service_lanes", C.c_uint64), ("last_denoise_ms", C.c_float), ("n_chunks", C.c_uint32),
                 ("n_passes", C.c_uint32), ("kernel", C.c_uint32), ("resampled", C.c_uint64), ("overflow_lost", C.c_uint64),
-                ("pair_cap", C.c_uint32), ("last_prepass_ms", C.c_float), ("last_main_ms", C.c_float)]
+                ("kernel_reason", C.c_uint32), ("last_prepass_ms", C.c_float), ("last_main_ms", C.c_float)]
 
 class GroupStats(C.Structure):
     _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
@@ -63,6 +63,8 @@ class GroupStats(C.Structure):
 _DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders"}   # may be absent from an older A/B build
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
+# rt_stats.kernel_reason (include/rt_capi.h RT_KERNEL_REASON_*)
+KERNEL_REASON_DEFAULT, KERNEL_REASON_TABLES_LDS, KERNEL_REASON_MATERIALS, KERNEL_REASON_MODE, KERNEL_REASON_KNOB = 0, 1, 2, 3, 4
 
 
 class DenoiseParams(C.Structure):

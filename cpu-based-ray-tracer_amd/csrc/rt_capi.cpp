@@ -133,6 +133,8 @@ constexpr size_t kMaxLdsScene = 48 * 1024;   // scenes up to ~700 triangles live
 constexpr size_t kMaxBvhSmallLds = 40 * 1024;
 constexpr uint32_t kStackDepth = 192;   // EXACT fold stack; RR 0.8 => P(depth > 192) ~ 2.5e-19 per sample
 constexpr uint32_t kStackDepthMax = 2048;
+// the vertex kernel's pending fold keeps its top ring position in 12 bits (rt_coherent.hip VS_PEND: top | count << 12)
+static_assert(kStackDepthMax <= 4096, "the pending fold's ring position is 12 bits (rt_coherent.hip VS_PEND)");
 constexpr uint32_t kResampleDepth = 4096;   // the kernels' path-length cap (P = rr^4096)
 
 // levels of the EXACT fold stack / ring for survival probability rr: 1.5 x the depth a path exceeds with
@@ -539,7 +541,11 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_lboxes, s->flat.lboxes)) != RT_OK) return r;
     if ((r = upload(c, c->d_sboxes, s->flat.sboxes)) != RT_OK) return r;
     if ((r = upload(c, c->d_stri, s->flat.stri)) != RT_OK) return r;
-    if ((r = upload(c, c->d_wcopies, s->flat.wcopies)) != RT_OK) return r;
+    {   // the near-first orderings (8 x the walked subtree's nodes: 40.7 MB at C5) only where the BVH variant walks them
+        static const std::vector<float> kNone;
+        const bool walks = c->vertex && c->vertex_bvh && c->split && c->walk_order && !c->qbvh && !c->force_walk;
+        if ((r = upload(c, c->d_wcopies, walks ? s->flat.wcopies : kNone)) != RT_OK) return r;
+    }
     c->split_root = s->flat.split_root;
     c->split_end = s->flat.split_end;
     c->n_sboxes = (uint32_t)(s->flat.sboxes.size() / 8);
@@ -776,6 +782,17 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31) &&
                          P.n_mats < (1u << 14) && bvh_small_bytes <= kMaxBvhSmallLds;
     const bool coh = coh_box || coh_bvh;
+    // why this kernel (rt_stats.kernel_reason; ADVICE r04: the BVH variant's LDS-table limit is a cliff the caller
+    // could not see)
+    uint32_t reason = RT_KERNEL_REASON_DEFAULT;
+    if (!coh && !whitted) {
+        if (count || c->gb_next) reason = RT_KERNEL_REASON_MODE;
+        else if (!c->vertex || (!c->vertex_bvh && !(P.n_lboxes > 0 && lds))) reason = RT_KERNEL_REASON_KNOB;
+        else if (P.n_mats >= (1u << 14)) reason = RT_KERNEL_REASON_MATERIALS;
+        else if (bvh_small_bytes > kMaxBvhSmallLds) reason = RT_KERNEL_REASON_TABLES_LDS;
+    } else if (coh_bvh && !c->brute && c->hdr.n_lboxes > 0) {
+        reason = RT_KERNEL_REASON_KNOB;   // RT_BRUTE=0: a small scene on the BVH variant
+    }
     // the camera pre-pass: the leaf-box variant always; the BVH variant for a split scene, whose camera rays are
     // traced like the path kernel's split phase (records carry the triangle in 19 bits, rt_kernels.h crec)
     const bool prepass = coh_box || (coh_bvh && c->bvh_prepass && P.split_root != 0u && P.n_tris < (1u << 19) - 1u);
@@ -807,7 +824,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (exact && !coh && c->lds_levels_force >= 0) P.lds_levels = std::min<uint32_t>((uint32_t)c->lds_levels_force, P.stack_depth);
     size_t shmem = ((lds || coh_bvh) ? (size_t)P.lds_scene_quads * sizeof(float4) : 0) + (exact ? rt_stack_lds_bytes(P.lds_levels) : 0) + lane_bytes + c->lds_pad;
     int bpc = occupancy(shmem);
-    c->stats.pair_cap = 0;
+    c->stats.kernel_reason = reason;
     if (bpc <= 0) bpc = c->occ_global[exact][count];
     uint32_t grid = c->n_cu * (uint32_t)bpc;
     if (exact) grid = std::min(grid, c->grid);   // the fold stack holds c->total_threads lanes
@@ -1214,6 +1231,40 @@ rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, in
     cleanup();
     c->pending_stats = true;   // last_kernel_ms = the trace kernel
     c->kev_used = 0;
+    return RT_OK;
+}
+
+rt_status rt_sample_light(rt_ctx* c, uint64_t n, const uint32_t* u, float* loc, float* normal, float* emission, float* pdf)
+{
+    if (!c || (n && (!u || !loc || !normal || !emission || !pdf))) return RT_ERR_INVALID;
+    if (!c->has_scene) { c->err = "no scene uploaded"; return RT_ERR_STATE; }
+    if (c->hdr.light_mesh < 0 || c->hdr.n_ltris == 0) { c->err = "the scene has no emissive mesh"; return RT_ERR_STATE; }
+    if (n == 0) return RT_OK;
+    if (n > 0x7FFFFFFFull) return RT_ERR_INVALID;
+    HIPC(c, hipSetDevice(c->device));
+    uint32_t* d_u = nullptr; float* d_out = nullptr;
+    auto cleanup = [&]() { dfree(d_u); dfree(d_out); };
+    KParams P{};
+    P.lnodes = c->d_lnodes; P.n_lnodes = c->hdr.n_lnodes;
+    P.ltris = c->d_ltris; P.n_ltris = c->hdr.n_ltris;
+    P.light_area = c->hdr.light_area;
+    std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
+    P.lpdf = 1.0f / c->hdr.light_area;   // as rt_render (an IEEE single division)
+    std::vector<float> out((size_t)n * 10);
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_u, n * 12)) != hipSuccess || (e = hipMalloc((void**)&d_out, n * 40)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_u, u, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = rt_launch_light_sample(P, (uint32_t)n, d_u, d_out, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(out.data(), d_out, n * 40, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_sample_light");
+    }
+    cleanup();
+    for (uint64_t i = 0; i < n; ++i) {
+        const float* o = &out[10 * i];
+        for (int k = 0; k < 3; ++k) { loc[3 * i + k] = o[k]; normal[3 * i + k] = o[3 + k]; emission[3 * i + k] = o[6 + k]; }
+        pdf[i] = o[9];
+    }
     return RT_OK;
 }
 

@@ -1242,6 +1242,10 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
 #endif
                 if (tracing) {
                     uint32_t ti = curA ? tiA : tiB;
+                    // a split scene's finite ray walks only the subtree [split_root, split_end) (its walk started at the
+                    // root; the nodes after the subtree hold outside leaves the split phase already tested): the DFS and
+                    // compact walks end at the subtree's end, as the near-first orderings do (their exit reads NN)
+                    const uint32_t tend = (kargs4().split_root != 0u && kargs4().force_walk == 0u && finite3(r.rcp)) ? kargs4().split_end : NN;
                     int parked0 = -1, parked1 = -1;
                     auto walk_q = [&]() {
                         // every node's quantized box (16 B): an internal hit descends, a leaf hit parks the
@@ -1249,7 +1253,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         const float ox = kargs4().q_origin[0], oy = kargs4().q_origin[1], oz = kargs4().q_origin[2];
                         const float sx = kargs4().q_scale[0], sy = kargs4().q_scale[1], sz = kargs4().q_scale[2];
                         const uint4* __restrict__ qn = kargs4().qnodes;
-                        for (uint32_t s = 0; s < steps && ti < NN; ++s) {
+                        for (uint32_t s = 0; s < steps && ti < tend; ++s) {
                             const uint4 q = qn[ti];
                             const float lx = __builtin_fmaf((float)(q.x & 0xFFFFu), sx, ox), hx = __builtin_fmaf((float)(q.x >> 16), sx, ox);
                             const float ly = __builtin_fmaf((float)(q.y & 0xFFFFu), sy, oy), hy = __builtin_fmaf((float)(q.y >> 16), sy, oy);
@@ -1270,7 +1274,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         const float4* wn = S.nodes;
                         if (Q.wcopies != nullptr && (decltype(kind)::value || finite3(r.rcp)))
                             wn = Q.wcopies + (((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) & Q.wcopy_mask) * Q.wcopy_stride;
-                        for (uint32_t s = 0; s < steps && ti < NN; ++s) {
+                        for (uint32_t s = 0; s < steps && ti < tend; ++s) {
                             const float4 q0 = wn[2 * ti];
                             const float4 q1 = wn[2 * ti + 1];
                             const bool hit = decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
@@ -1321,6 +1325,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             }
                         }
                     }
+                    if (ti >= tend) ti = NN;
                     if (curA) tiA = ti;
                     else tiB = ti;
                     SEC_MARK(5);

@@ -677,6 +677,37 @@ hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const
 }
 
 // ---------------------------------------------------------------------------------------------
+// light-sampling query kernel (C-ABI rt_sample_light: Renderer::SamplingAreaLight of the drop-in,
+// MC/Renderer.h:163-180): the path kernels' sample_light on three given u32 draws per case
+struct GivenDraws {
+    const uint32_t* u;
+    uint32_t k;
+    __device__ __forceinline__ float next() { return (float)u[k++] / 4294967296.0f; }   // Walnut::Random::Float (WN/Random.h:27-30)
+};
+
+__global__ void __launch_bounds__(256) light_sample_kernel(KParams P, uint32_t n, const uint32_t* __restrict__ u, float* __restrict__ out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SceneView S{P.nodes, P.tris, P.mats, P.lnodes, P.ltris, P.n_nodes, P.lboxes};
+    GivenDraws g{u + 3 * (size_t)i, 0u};
+    V3 q, nl;
+    sample_light(S, P.light_area, g, q, nl);
+    float* o = out + 10 * (size_t)i;
+    o[0] = q.x; o[1] = q.y; o[2] = q.z;
+    o[3] = nl.x; o[4] = nl.y; o[5] = nl.z;
+    o[6] = P.light_emission[0]; o[7] = P.light_emission[1]; o[8] = P.light_emission[2];
+    o[9] = P.lpdf;   // the PDF Sampling_from_root overwrites with 1 / (the light's total area), MC/BVH.h:105-106
+}
+
+hipError_t rt_launch_light_sample(const KParams& P, uint32_t n, const uint32_t* u, float* out, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(light_sample_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, P, n, u, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // math self-test kernel: device f32 sqrt/div, f64 reciprocal, cos/sin as the megakernel evaluates them,
 // and the denoiser's expf/acosf (rt_glibc_math.h)
 __global__ void math_kernel(uint32_t n, const float* __restrict__ x, float* __restrict__ out)

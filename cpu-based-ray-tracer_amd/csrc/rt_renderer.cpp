@@ -196,6 +196,7 @@ Renderer::~Renderer()
 {
     rt_group_destroy(group);
     rt_destroy(ctx);
+    rt_destroy(qctx);
     rt_scene_destroy(scene_);
 }
 
@@ -217,6 +218,62 @@ void Renderer::GenerateBVH()
     rt_scene_destroy(scene_);
     scene_ = sc;   // kept for Scene()
     bvh_dirty = false;
+    qctx_stale = true;
+    // the per-triangle records the queries return (face normal, mesh)
+    rt_scene_info info{};
+    check(rt_scene_get_info(sc, &info), "rt_scene_get_info");
+    std::vector<float> nf((size_t)info.n_nodes * 7), tf((size_t)info.n_tris * 13);
+    std::vector<int32_t> ni((size_t)info.n_nodes * 5), ti((size_t)info.n_tris * 2);
+    check(rt_scene_export(sc, nf.data(), ni.data(), tf.data(), ti.data()), "rt_scene_export");
+    tri_normal_.resize((size_t)info.n_tris * 3);
+    tri_mesh_.resize(info.n_tris);
+    for (size_t i = 0; i < info.n_tris; ++i) {
+        for (int k = 0; k < 3; ++k) tri_normal_[3 * i + k] = tf[13 * i + 9 + k];
+        tri_mesh_[i] = ti[2 * i];
+    }
+}
+
+rt_ctx* Renderer::query_ctx() const
+{
+    if (ctx) return ctx;
+    if (!qctx) {
+        rt_device_cfg cfg{settings.devices.empty() ? settings.device : settings.devices[0], nullptr, 0};
+        check(rt_create(&qctx, &cfg), "rt_create");
+        qctx_stale = true;
+    }
+    if (qctx_stale) {
+        const rt_status st = rt_upload_scene(qctx, scene_);
+        if (st != RT_OK) throw rt::Error(std::string("rt_upload_scene failed: ") + rt_last_error(qctx));
+        qctx_stale = false;
+    }
+    return qctx;
+}
+
+Renderer::Hit Renderer::Trace(const vec3& origin, const vec3& direction) const
+{
+    if (bvh_dirty || !scene_) throw rt::Error("ray_BVH_intersection_record before GenerateBVH");
+    rt_ctx* q = query_ctx();
+    const float o[3] = {origin.x, origin.y, origin.z}, d[3] = {direction.x, direction.y, direction.z};
+    int32_t tri = -1;
+    double t = 0.0;
+    const rt_status st = rt_trace(q, 1, o, d, &tri, &t);
+    if (st != RT_OK) throw rt::Error(std::string("rt_trace failed: ") + rt_last_error(q));
+    Hit h;
+    if (tri >= 0 && (size_t)tri < tri_mesh_.size()) {
+        h.hit = true; h.t = t; h.triangle = tri; h.mesh = tri_mesh_[tri];
+        h.normal = vec3{tri_normal_[3 * tri], tri_normal_[3 * tri + 1], tri_normal_[3 * tri + 2]};
+    }
+    return h;
+}
+
+Renderer::LightSample Renderer::SampleLight(const uint32_t draws[3]) const
+{
+    if (bvh_dirty || !scene_) throw rt::Error("SamplingAreaLight before GenerateBVH");
+    rt_ctx* q = query_ctx();
+    float loc[3], n[3], em[3], pdf = 0.0f;
+    const rt_status st = rt_sample_light(q, 1, draws, loc, n, em, &pdf);
+    if (st != RT_OK) throw rt::Error(std::string("rt_sample_light failed: ") + rt_last_error(q));
+    return LightSample{vec3{loc[0], loc[1], loc[2]}, vec3{n[0], n[1], n[2]}, vec3{em[0], em[1], em[2]}, pdf};
 }
 
 void Renderer::ResizeViewport(uint32_t width, uint32_t height)

@@ -26,13 +26,16 @@ def local_rows(H, band, rank, nranks):
 class ImageGather:
     """Preallocated all-gather of per-rank RGBA8 row sets + reassembly on rank 0."""
 
-    def __init__(self, W, H, band, rank, nranks, device):
+    def __init__(self, W, H, band, rank, nranks, device, collective=None):
+        """collective: run the all-gather even with one rank (bench.py --force-dist: the RCCL path exercised on a
+        one-GPU box); default: only when nranks > 1."""
         self.W, self.H, self.rank, self.nranks = W, H, rank, nranks
+        self.collective = nranks > 1 if collective is None else bool(collective)
         rows = [local_rows(H, band, r, nranks) for r in range(nranks)]
         self.max_rows = max(len(r) for r in rows)
         self.n_local = len(rows[rank])
         self.send = torch.zeros(self.max_rows * W, dtype=torch.int32, device=device)
-        self.recv = torch.zeros(nranks * self.max_rows * W, dtype=torch.int32, device=device) if nranks > 1 else self.send
+        self.recv = torch.zeros(nranks * self.max_rows * W, dtype=torch.int32, device=device) if self.collective else self.send
         self.image = torch.zeros(H * W, dtype=torch.int32, device=device)
         src, dst = [], []
         for r in range(nranks):
@@ -48,7 +51,7 @@ class ImageGather:
 
     def gather(self):
         """All-gather the row sets; rank 0 scatters them into image (H*W int32, row 0 = bottom)."""
-        if self.nranks > 1:
+        if self.collective:
             if self.send.is_cuda:
                 dist.all_gather_into_tensor(self.recv, self.send)
             else:   # gloo has no all_gather_into_tensor on every torch build

@@ -96,6 +96,19 @@ public:
     // check a scene built through Add against the reference's BVH
     const rt_scene* Scene() const { return scene_; }
 
+    // The reference Renderer's scene queries on the scene of the last GenerateBVH, answered by this library's
+    // device kernels (rt_trace / rt_sample_light: the path kernels' own traversal and light sampling).  One ray
+    // or one sample per call, a kernel launch and a synchronisation each; batch through the C-ABI for many.
+    // ray_BVH_intersection_record (MC/Renderer.h:88-91 -> BVH::traverse_BVH_from_root, MC/BVH.h:72-101):
+    // the closest hit's double t, its triangle (flattened slot), the mesh it belongs to (index into
+    // GetEntities()) and the triangle's face normal (MC/TriangleMesh.h:57-59,118-134)
+    struct Hit { bool hit = false; double t = 1.7976931348623157e308; int32_t triangle = -1; int32_t mesh = -1; vec3 normal{}; };
+    Hit Trace(const vec3& origin, const vec3& direction) const;
+    // SamplingAreaLight (MC/Renderer.h:163-180) on three given Walnut::Random words (area pick, triangle x,
+    // triangle y): the point, the light triangle's normal, the light's emission and PDF = 1 / total light area
+    struct LightSample { vec3 location, normal, emission; float pdf = 0.0f; };
+    LightSample SampleLight(const uint32_t draws[3]) const;
+
     float RR_survival_probability = 0.8f;        // MC/Renderer.h:199
     std::vector<rt::Entity*> entities;
 
@@ -111,6 +124,12 @@ private:
     std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
     rt_scene* scene_ = nullptr;
     bool bvh_dirty = true;
+    // the queries' context: ctx, or (several devices) one on the first device holding the scene
+    rt_ctx* query_ctx() const;
+    mutable rt_ctx* qctx = nullptr;
+    mutable bool qctx_stale = true;
+    std::vector<float> tri_normal_;    // per flattened triangle: face normal (rt_scene_export)
+    std::vector<int32_t> tri_mesh_;    // per flattened triangle: mesh index
 };
 
 }  // namespace rt

@@ -21,7 +21,11 @@
 #ifndef RT_NO_GLOBAL_NAMES
 #define RT_NO_GLOBAL_NAMES
 #endif
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
+#include <limits>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -61,6 +65,41 @@ public:
 // the path tracer's entities are triangle meshes (MC/Entity.h's interface is the renderer's business here)
 using Entity = rt::Entity;
 
+// Whitted::IntersectionRecord, MC/IntersectionRecord.h:18-38 (what ray_BVH_intersection_record and
+// SamplingAreaLight of the drop-in Renderer return).  hitted_entity is the hit MESH (the flattened scene has
+// no per-triangle entity objects; the reference points at its TrianglePrimitive), hitted_entity_material the
+// mesh's material.
+class IntersectionRecord {
+public:
+    bool has_intersection = false;
+    double t = std::numeric_limits<double>::max();
+    glm::vec3 location{0.0f, 0.0f, 0.0f};
+    glm::vec3 surface_normal{0.0f, 0.0f, 0.0f};
+    glm::vec3 emission{0.0f, 0.0f, 0.0f};
+    Entity* hitted_entity = nullptr;
+    WhittedMaterial* hitted_entity_material = nullptr;
+};
+
+// MC/WhittedUtilities.h:18-30
+#ifndef INTERSECTION_CORRECTION
+#define INTERSECTION_CORRECTION 0.00001f
+#endif
+inline float clamp_float(const float& value, const float& lower_bound, const float& upper_bound)
+{
+    return std::max(std::min(value, upper_bound), lower_bound);
+}
+
+// Walnut::Random as the reference's platform (MSVC) runs it (WN/Random.h:27-48, WN/Random.cpp:5-6): a
+// thread_local std::mt19937 with its default seed, drawn through a 32-bit uniform distribution, so one draw is
+// one engine word; Float() = (float)word / (float)UINT32_MAX.  get_random_float_0_1 is MC/WhittedUtilities.h:23-26.
+inline std::mt19937& random_engine()
+{
+    static thread_local std::mt19937 engine;
+    return engine;
+}
+inline uint32_t get_random_u32() { return (uint32_t)random_engine()(); }
+inline float get_random_float_0_1() { return (float)get_random_u32() / (float)UINT32_MAX; }
+
 class TriangleMesh : public rt::Entity {   // MC/TriangleMesh.h:144-267
 public:
     TriangleMesh(const std::string& file_path, WhittedMaterial* m) : mesh_(file_path, rt::Material{}), unified_material(m) {}
@@ -73,6 +112,7 @@ public:
         return material_;
     }
     bool IsEmissive() { return unified_material->IsEmitting(); }   // MC/TriangleMesh.h:198-201
+    WhittedMaterial* UnifiedMaterial() const { return unified_material; }   // (private in the reference)
 
 private:
     rt::TriangleMesh mesh_;

@@ -36,7 +36,7 @@ extern "C" {
 
 /* 2 (round 4): rt_stats grew last_prepass_ms / last_main_ms, rt_scene_info the light-skip and split fields,
  * rt_read_accumulation was added; a host built against another version must not pass its structs */
-#define RT_API_VERSION 2
+#define RT_API_VERSION 3
 
 typedef int32_t rt_status;
 #define RT_OK 0
@@ -233,7 +233,8 @@ typedef struct {
     uint64_t resampled;       /* EXACT: samples whose path outgrew the fold ring, rendered again exactly */
     uint64_t overflow_lost;   /* EXACT: levels / samples that could not be kept (non-zero => RT_ERR_OVERFLOW)
                                  -- both summed over the renders since the last synchronisation that checked them */
-    uint32_t pair_cap;        /* reserved (0): the wave-spread Moller-Trumbore pair list was removed */
+    uint32_t kernel_reason;   /* why `kernel` rendered the last path frame: RT_KERNEL_REASON_* (API 3; was a reserved
+                                 zero in API 2) */
     float last_prepass_ms;    /* the vertex kernel's camera pre-pass (camera_prepass_kernel), summed over passes */
     float last_main_ms;       /* the path kernel proper (pt_coherent_kernel / pt_megakernel), summed over passes;
                                  last_kernel_ms spans these plus the resample and in-order finalize kernels */
@@ -242,6 +243,13 @@ typedef struct {
 #define RT_KERNEL_VERTEX 1    /* pt_coherent_kernel (rt_coherent.hip): small scenes, vertex-synchronous */
 #define RT_KERNEL_WHITTED 2   /* whitted_kernel / whitted_world_kernel (rt_whitted.hip) */
 #define RT_KERNEL_VERTEX_BVH 3   /* pt_coherent_kernel's BVH variant (rt_coherent.hip): other path scenes */
+#define RT_KERNEL_REASON_DEFAULT 0       /* the kernel the scene calls for */
+#define RT_KERNEL_REASON_TABLES_LDS 1    /* megakernel: the BVH variant stages the material and light tables (and a
+                                            split scene's outside triangles) in LDS, and they exceed its 40 KB
+                                            (about 2500 light triangles or 1280 materials); a large slowdown */
+#define RT_KERNEL_REASON_MATERIALS 2     /* megakernel: 2^14 materials or more (the vertex kernel packs 14 bits) */
+#define RT_KERNEL_REASON_MODE 3          /* megakernel: a work-counter render or a denoiser G-buffer frame */
+#define RT_KERNEL_REASON_KNOB 4          /* a debug knob (RT_VERTEX / RT_VERTEX_BVH / RT_BRUTE) chose it */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 /* diagnostic: the raw device counters of the last rt_render (up to 512 x u64; [16..23] = wave cycles per
  * section and [24..43] = wave-level event counts of the vertex kernel in RT_SECTIONS builds, [64..511]
@@ -312,6 +320,12 @@ rt_status rt_get_gbuffer(rt_ctx* ctx, float* color, float* position, float* norm
 
 /* closest hit of n rays (host arrays; tri = flattened triangle slot or -1, t = double distance) */
 rt_status rt_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* tri, double* t);
+/* Renderer::SamplingAreaLight (MC/Renderer.h:163-180 -> TriangleMesh::Sampling -> BVH::Sampling_from_root,
+ * MC/TriangleMesh.h:193-197, MC/BVH.h:103-129, MC/TriangleMesh.h:69-89) on the device, for n cases of three
+ * given u32 draws (Walnut::Random::Float's words: area pick, triangle x, triangle y): the sampled location and
+ * the light triangle's normal (3 floats each), the light's emission (3 floats) and the PDF 1 / total light
+ * area (the overwrite of MC/BVH.h:105-106).  RT_ERR_STATE if the scene has no emissive mesh. */
+rt_status rt_sample_light(rt_ctx* ctx, uint64_t n, const uint32_t* u, float* loc, float* normal, float* emission, float* pdf);
 /* closest hit of n rays against a Whitted world (get_intersection_payload, WH/Renderer.h:109-140):
  * entity index or -1, mesh triangle slot or -1, and (t, barycentric 2, barycentric 3) as 3 floats */
 rt_status rt_world_trace(rt_ctx* ctx, uint64_t n, const float* org, const float* dir, int32_t* entity, int32_t* tri, float* t_bary);

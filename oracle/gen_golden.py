@@ -10,9 +10,12 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py bvh        # only the BVH Ray Tracer (C3) fixtures
     python oracle/gen_golden.py dn         # only the Denoiser project fixtures
     python oracle/gen_golden.py c1         # only the C1 (Whitted two-sphere world) fixtures
+    python oracle/gen_golden.py optics     # only the Renderer optics helpers (mirror / Snell / Fresnel)
     python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
     python oracle/gen_golden.py full       # C2 and C4 at their full spp (full_c2 / full_c4: one of them)
+    python oracle/gen_golden.py full_c5    # C5 (Cornell + 79k-triangle bunny) at 3840x2160x256 (~10 min)
+    python oracle/gen_golden.py full_c5_4096  # C5 at its full 4096 spp (hours; background job)
 """
 import os
 import subprocess
@@ -267,6 +270,46 @@ def gen_full(which=None):
                             rgba_rows=np.ascontiguousarray(rgba[rows]), stats=np.fromfile(tmp("stats"), "<u8"))
 
 
+C5_FULL_ROW_STRIDE = 64
+
+
+def c5_obj():
+    """The C5 OBJ (the bunny subdivided 1:4 twice, written x100), as gen_c5 makes it."""
+    rt = load_pkg()
+    bunny = np.load(os.path.join(GOLDEN, "bvh_scene.npz"))["raw_bunny"]
+    raw = rt.c5_mesh(bunny)
+    obj = tmp("c5_bunny.obj")
+    rt.write_obj(obj, raw)
+    return obj
+
+
+def gen_full_c5(spp=256):
+    """C5's launch shape: the Cornell box + the 79,488-triangle bunny at 3840x2160,
+    seed 0, RR 0.8, frames 1..spp, through the reference's own TriangleMesh + BVH (MC/Renderer.cpp:114-133
+    accumulation over all frames; MC/BVH.h:72-101 traversal).  2.1 G samples at 256 spp: long enough that
+    some paths exceed the 624 words of one engine fill, so the harness re-fills the injected stream at the
+    top of a shading call (mt_inject.h refill_if_near).  Stores the SHA-256 of the float4 accumulation and
+    of the RGBA8 frame, and every 64th row of the accumulation's rgb."""
+    import hashlib
+    import time
+    W, H = 3840, 2160
+    obj = c5_obj()
+    t0 = time.time()
+    run("image", CORNELL_DIR, obj, W, H, spp, 0, 0.8, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+    secs = time.time() - t0
+    acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+    rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+    rows = np.arange(0, H, C5_FULL_ROW_STRIDE)
+    name = "full_c5" if spp == 256 else f"full_c5_{spp}"
+    np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), W=np.int64(W), H=np.int64(H), spp=np.int64(spp),
+                        seed=np.int64(0), rr=np.float32(0.8), first_frame=np.int64(1),
+                        sha_accum=np.array(hashlib.sha256(acc.tobytes()).hexdigest()),
+                        sha_rgba=np.array(hashlib.sha256(rgba.tobytes()).hexdigest()),
+                        rows=rows.astype(np.int64), accum_rows=np.ascontiguousarray(acc[rows, :, :3]),
+                        rgba_rows=np.ascontiguousarray(rgba[rows]), stats=np.fromfile(tmp("stats"), "<u8"),
+                        harness_seconds=np.float64(secs), harness_threads=np.int64(os.cpu_count() or 8))
+
+
 def gen_stat():
     """The reference with its SHIPPED random stream (serial std::mt19937 seeded 5489, MSVC 32-bit
     distribution, camera draws then pixel loop per frame): the statistical gate of SURVEY.md 8(d)."""
@@ -453,6 +496,27 @@ HARNESS_WH = os.path.join(HERE, "_ref", "ref_whitted_spheres")
 WH_HIT_DT = np.dtype([("ent", "<i4"), ("tri", "<i4"), ("t", "<f4"), ("b2", "<f4"), ("b3", "<f4")])
 
 
+def gen_optics(rng):
+    """The Renderer's optics helpers (mirror_reflection_direction, snell_refraction_direction,
+    accurate_fresnel_reflectance: WH/Renderer.h:41-107, the same code as MC/Renderer.h:93-161) on unit incident
+    directions and normals from outside and inside, grazing and perpendicular incidence, and total internal
+    reflection, for the drop-in Renderer's public surface (tests/test_walnut_queries.py)."""
+    n = 4096
+    def unit(k):
+        v = rng.normal(size=(k, 3))
+        return (v / np.linalg.norm(v, axis=1, keepdims=True)).astype(np.float32)
+    I, N = unit(n), unit(n)
+    eta = rng.choice(np.array([1.0, 1.00029, 1.333, 1.5, 1.6, 2.42, 0.75], np.float32), n).astype(np.float32)
+    # exact edge cases: I perpendicular to N (cos 0: "inside"), I = -N, I = N, axis-aligned normals
+    I[:4] = [[1, 0, 0], [0, -1, 0], [0, 1, 0], [0.6, -0.8, 0]]
+    N[:4] = [[0, 1, 0], [0, 1, 0], [0, 1, 0], [0, 1, 0]]
+    cases = np.concatenate([I, N, eta[:, None]], 1).astype("<f4")
+    cases.tofile(tmp("optics.in"))
+    run_wh("optics", tmp("optics.in"), tmp("optics.out"))
+    res = np.fromfile(tmp("optics.out"), "<f4").reshape(n, 7)
+    np.savez_compressed(os.path.join(GOLDEN, "optics_cases.npz"), cases=cases, mirror=res[:, 0:3], snell=res[:, 3:6], fresnel=res[:, 6])
+
+
 def run_wh(*args):
     r = subprocess.run([HARNESS_WH] + [str(a) for a in args], capture_output=True, text=True)
     if r.returncode != 0:
@@ -591,12 +655,18 @@ def main():
             gen_bvh_images()
         if only in ("all", "c1"):
             gen_c1(np.random.default_rng(20261017))
+        if only in ("all", "c1", "optics"):
+            gen_optics(np.random.default_rng(20261018))
         if only in ("all", "dn"):
             gen_dn()
         if only in ("all", "c5"):
             gen_c5(np.random.default_rng(20261016))
         if only in ("all", "full", "full_c2", "full_c4"):
             gen_full(None if only in ("all", "full") else only[5:])
+        if only == "full_c5":
+            gen_full_c5(256)
+        if only == "full_c5_4096":
+            gen_full_c5(4096)
     print("golden fixtures written to", GOLDEN)
 
 

@@ -42,13 +42,15 @@ struct Injector {
     uint64_t seed = 0;
     uint32_t pixel = 0, frame = 0;
     uint32_t filled = 0;
+    uint32_t base = 0;   // stream index of engine word 0 (non-zero after a refill)
     std::mt19937::result_type x0 = 0;
-    void start(uint64_t s, uint32_t px, uint32_t fr, uint32_t n)
+    void start(uint64_t s, uint32_t px, uint32_t fr, uint32_t n) { seed = s; pixel = px; frame = fr; fill(0, n); }
+    void fill(uint32_t from, uint32_t n)
     {
-        seed = s; pixel = px; frame = fr;
         MTLayout l;
         if (n > 624) n = 624;
-        for (uint32_t i = 0; i < n; ++i) l.x[i] = mt_untemper(oracle_rng_u32(seed, pixel, frame, i));
+        base = from;
+        for (uint32_t i = 0; i < n; ++i) l.x[i] = mt_untemper(oracle_rng_u32(seed, pixel, frame, from + i));
         // past the filled prefix: all-ones draws (Float()==1.0f ends the path at the next RR test);
         // a path that still exhausts the engine triggers a twist, detected through x[0] in used()
         for (uint32_t i = n; i < 624; ++i) l.x[i] = mt_untemper(0xFFFFFFFFu);
@@ -57,16 +59,42 @@ struct Injector {
         x0 = l.x[0];
         std::memcpy((void*)&Walnut::Random::s_RandomEngine, &l, sizeof l);
     }
-    // number of draws consumed; 0xFFFFFFFF if the engine twisted (more than 624 draws)
+    // number of draws consumed since start(); 0xFFFFFFFF if the engine twisted (more than the filled
+    // words were drawn without a refill)
     uint32_t used() const
     {
         MTLayout l;
         std::memcpy(&l, (const void*)&Walnut::Random::s_RandomEngine, sizeof l);
         if (l.x[0] != x0) return 0xFFFFFFFFu;
-        return (uint32_t)l.p;
+        return base + (uint32_t)l.p;
     }
+    // Called by the harness glue where the next `need` draws are about to be taken (the top of a
+    // shading call, which draws at most 6).  If they would run past the filled words, the engine is
+    // re-filled with the stream's next `g_fill_words` words (624 unless RT_HARNESS_FILL says fewer, a
+    // self-check of this very mechanism) and its position reset, so a path of any length reads the
+    // counter-based stream and the engine never twists.
+    void refill_if_near(uint32_t need);
 };
 static thread_local Injector g_inj;
+static uint32_t g_fill_words = 624;
+
+inline void Injector::refill_if_near(uint32_t need)
+{
+    if (filled == 0) return;   // not injecting (the shipped-stream modes)
+    MTLayout l;
+    std::memcpy(&l, (const void*)&Walnut::Random::s_RandomEngine, sizeof l);
+    if (l.x[0] != x0) return;   // already twisted: used() reports it
+    if ((uint32_t)l.p + need <= filled) return;
+    fill(base + (uint32_t)l.p, g_fill_words);
+}
+
+static void read_fill_words()
+{
+    if (const char* e = getenv("RT_HARNESS_FILL")) {
+        long v = atol(e);
+        if (v >= 8 && v <= 624) g_fill_words = (uint32_t)v;
+    }
+}
 
 static void set_msvc_distribution()
 {

@@ -189,6 +189,7 @@ struct Hybrid {
     glm::vec3 shading(const Whitted::IntersectionRecord& record, const glm::vec3& W_out) const
     {   // Renderer::shading, MC/Renderer.cpp:148-214
         g_cnt.shading++;
+        g_inj.refill_if_near(6);   // harness: keep the injected stream from twisting (mt_inject.h)
         if (record.hitted_entity_material->IsEmitting()) return record.hitted_entity_material->GetEmission();
         glm::vec3 n = record.surface_normal;
         if (glm::dot(record.surface_normal, W_out) < 0.0f) n = -(record.surface_normal);
@@ -435,20 +436,16 @@ static int cmd_image(const char* dir, const char* extra, uint32_t W, uint32_t H,
                 uint32_t px = y * W + x;
                 glm::vec4 acc{0.0f};
                 for (uint32_t f = 1; f <= spp; ++f) {
-                    uint32_t want = 64, used = 0;
-                    glm::vec3 L;
-                    for (;;) {
-                        g_cnt = Counters{};
-                        g_inj.start(seed, px, f, want);
-                        // RayGen_Shader, MC/Renderer.cpp:124-134 (camera direction drawn first, as
-                        // UpdateCamera -> RecomputeRayDirections precedes Render, MC/mainloop.cpp:32-41)
-                        glm::vec3 dir = camera_dir(cam, x, y, W, H);
-                        L = h.cast_path(AccelerationStructure::Ray{cam.Position(), Whitted::normalize(dir)});
-                        used = g_inj.used();
-                        if (used <= want) break;
-                        if (want == 624) { overflow++; used = 624; break; }
-                        want = 624;
-                    }
+                    // A first fill of 64 words covers nearly every path; a longer one is re-filled at
+                    // the top of a shading call (mt_inject.h refill_if_near), so the engine never twists.
+                    g_cnt = Counters{};
+                    g_inj.start(seed, px, f, std::min<uint32_t>(64, g_fill_words));
+                    // RayGen_Shader, MC/Renderer.cpp:124-134 (camera direction drawn first, as
+                    // UpdateCamera -> RecomputeRayDirections precedes Render, MC/mainloop.cpp:32-41)
+                    glm::vec3 dir = camera_dir(cam, x, y, W, H);
+                    glm::vec3 L = h.cast_path(AccelerationStructure::Ray{cam.Position(), Whitted::normalize(dir)});
+                    uint32_t used = g_inj.used();
+                    if (used == 0xFFFFFFFFu) { overflow++; used = 0; }
                     local.rays += g_cnt.rays; local.shading += g_cnt.shading; local.draws += used;
                     glm::vec4 color_rgba{L, 1.0f};
                     acc += color_rgba;
@@ -485,6 +482,7 @@ static int cmd_image_mt(const char* dir, uint32_t W, uint32_t H, uint32_t spp, f
     cam.ResizeViewport(W, H);
     Walnut::Random::s_RandomEngine.seed(5489u);
     set_msvc_distribution();
+    read_fill_words();
     Hybrid h{s, rr};
     std::vector<glm::vec4> acc((size_t)W * H, glm::vec4(0.0f));
     std::vector<glm::vec3> dirs((size_t)W * H);
@@ -565,6 +563,7 @@ int main(int argc, char** argv)
 {
     check_layout_once();
     set_msvc_distribution();
+    read_fill_words();
     if (argc < 2) { fprintf(stderr, "usage: ref_harness <cmd> ...\n"); return 1; }
     std::string c = argv[1];
     if (c == "scene" && argc == 7) return cmd_scene(argv[2], argv[3], argv[4], argv[5], argv[6]);

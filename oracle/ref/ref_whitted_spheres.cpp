@@ -281,6 +281,22 @@ int cmd_pow(const char* in, const char* out)
     return 0;
 }
 
+// the Renderer's optics helpers (WH/Renderer.h:41-107; MC/Renderer.h:93-161 is the same code as const members) on
+// (incident xyz, normal xyz, eta) cases -> mirror xyz, snell xyz, fresnel: the drop-in Renderer's fixtures
+int cmd_optics(const char* in, const char* out)
+{
+    auto v = read_all<float>(in);
+    Out o(out);
+    for (size_t i = 0; i + 6 < v.size(); i += 7) {
+        const glm::vec3 I{v[i], v[i + 1], v[i + 2]}, N{v[i + 3], v[i + 4], v[i + 5]};
+        const float eta = v[i + 6];
+        const glm::vec3 m = mirror_reflection_direction(I, N), t = snell_refraction_direction(I, N, eta);
+        o.put(m.x); o.put(m.y); o.put(m.z); o.put(t.x); o.put(t.y); o.put(t.z); o.put(accurate_fresnel_reflectance(I, N, eta));
+    }
+    printf("optics %zu\n", v.size() / 7);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -290,6 +306,7 @@ int main(int argc, char** argv)
     if (c == "camera" && argc == 5) return cmd_camera(atoi(argv[2]), atoi(argv[3]), argv[4]);
     if (c == "rays" && argc == 4) return cmd_rays(argv[2], argv[3]);
     if (c == "pow" && argc == 4) return cmd_pow(argv[2], argv[3]);
+    if (c == "optics" && argc == 4) return cmd_optics(argv[2], argv[3]);
     if (c == "image" && argc == 9) return cmd_image(atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), argv[6], argv[7], argv[8]);
     fprintf(stderr, "bad command\n");
     return 1;

@@ -129,6 +129,10 @@ def main():
             out[name.lower().replace("sq_insts_", "") + "_wave_insts_per_sample"] = counters[name] / args.samples
     if "SQ_THREAD_CYCLES_VALU" in counters and "SQ_INSTS_VALU" in counters:
         out["valu_lane_utilization"] = counters["SQ_THREAD_CYCLES_VALU"] / (64 * counters["SQ_INSTS_VALU"])
+    if "SQ_WAIT_ANY" in counters and "SQ_WAVE_CYCLES" in counters and counters["SQ_WAVE_CYCLES"]:
+        out["wait_any_frac"] = counters["SQ_WAIT_ANY"] / counters["SQ_WAVE_CYCLES"]
+    if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters and (counters["TCC_HIT_sum"] + counters["TCC_MISS_sum"]):
+        out["l2_hit_rate"] = counters["TCC_HIT_sum"] / (counters["TCC_HIT_sum"] + counters["TCC_MISS_sum"])
     if "SQ_INSTS_VALU" in counters and "GRBM_GUI_ACTIVE" in counters:
         # VALU issue slots used: wave-instructions x 2 cycles over all SIMDs' cycles (GRBM_GUI_ACTIVE is
         # summed over the 8 XCDs)

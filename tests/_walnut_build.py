@@ -8,7 +8,9 @@
    box runs the binary built here (tests/_bin/, git-ignored, shipped with the tree like the .so files).
 2. tests/walnut_stub/c5_scene.cpp: configuration C5 built through the reference's scene-extension spelling
    (Whitted::WhittedMaterial, Whitted::TriangleMesh(path, material*), Add, GenerateBVH) against the same
-   drop-in headers.  Needs no reference file."""
+   drop-in headers.  Needs no reference file.
+3. tests/walnut_stub/queries.cpp: the drop-in Renderer's scene queries and optics helpers with the reference's
+   signatures (MC/Renderer.h:88-180).  Needs no reference file."""
 import os
 import shutil
 import subprocess
@@ -18,6 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MAINLOOP = "/root/reference/Monte Carlo Path Tracer/8599RayTracerGUI/src/mainloop.cpp"
 BIN = os.path.join(REPO, "tests", "_bin", "walnut_mainloop")
 C5_BIN = os.path.join(REPO, "tests", "_bin", "walnut_c5_scene")
+QUERIES_BIN = os.path.join(REPO, "tests", "_bin", "walnut_queries")
 STUB = os.path.join(REPO, "tests", "walnut_stub")
 PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
 
@@ -35,8 +38,13 @@ def build_c5(out=C5_BIN):
     return _gxx([os.path.join(STUB, "c5_scene.cpp")], out)
 
 
+def build_queries(out=QUERIES_BIN):
+    return _gxx([os.path.join(STUB, "queries.cpp")], out)
+
+
 def build(out=BIN):
     build_c5(os.path.join(os.path.dirname(out), os.path.basename(C5_BIN)))
+    build_queries(os.path.join(os.path.dirname(out), os.path.basename(QUERIES_BIN)))
     if not os.path.exists(MAINLOOP):
         return None
     tmp = tempfile.mkdtemp(prefix="rt_walnut_")

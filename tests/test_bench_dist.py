@@ -58,3 +58,38 @@ def test_bench_gloo_matches_one_rank(tmp_path, world, W, H):
     finally:
         c.close()
     assert np.array_equal(gathered, np.ascontiguousarray(one).view(np.uint32).reshape(H, W))
+
+
+@pytest.mark.parametrize("W,H,spp", [(W, H, SPP), (1920, 1080, 1024)], ids=["small", "c4"])
+def test_bench_rccl_branch_one_rank(tmp_path, W, H, spp):
+    """bench.py's RCCL branch executed, not emulated -- torch.distributed.run with ONE rank
+    and --force-dist: init_process_group("nccl"), dist.py's all_gather_into_tensor of the RGBA8 bands on
+    device tensors, the all_gather of the rank times and the MAX all_reduce, the barriers, and (at the C4
+    shape) frame_parity's all_reduces over RCCL.  Not a scaling claim: one rank, one GPU.  The JSON line
+    must report the collectives and the gathered frame must equal a plain render bit for bit."""
+    img = tmp_path / "frame.npy"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "1", "--force-dist", "--dist-backend", "nccl",
+           "--steps", "2", "--warmup", "1", "--width", str(W), "--height", str(H), "--spp", str(spp), "--no-cpu-baseline",
+           "--no-fast-probe", "--dump-image", str(img)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["config"]["dist_backend"] == "nccl"
+    assert line["collectives"]["backend"] == "nccl" and line["collectives"]["forced_one_rank"] is True
+    assert len(line["rank_elapsed_s"]) == 1
+    assert abs(line["value"] - W * H * spp * 2 / line["rank_elapsed_s"][0] / 1e6) <= 1e-2 * line["value"]
+    if spp == 1024:
+        assert line["parity"]["sha_match"] is True and line["parity"]["rmse_vs_ref"] == 0.0
+    gathered = np.load(img)
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        cam, _, _ = rt.camera_default(W, H)
+        one, _ = c.render(cam, spp, seed=0)
+    finally:
+        c.close()
+    assert np.array_equal(gathered, np.ascontiguousarray(one).view(np.uint32).reshape(H, W))

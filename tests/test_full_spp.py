@@ -59,7 +59,7 @@ def test_full_spp_frame_matches_reference(name):
         cam, _, _ = rt.camera_default(W, H)
         rgba, acc = c.render(cam, spp, first_frame=1, seed=0, rr=0.8)
         st = c.stats()
-        assert st.kernel == 1 and st.overflow_lost == 0
+        assert st.kernel == 1 and st.overflow_lost == 0 and st.kernel_reason == rt.KERNEL_REASON_DEFAULT
     finally:
         c.close()
     rows = acc[z["rows"], :, :3]

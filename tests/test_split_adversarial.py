@@ -169,7 +169,9 @@ def test_light_tables_beyond_lds_take_the_megakernel():
         c.resize(W, H)
         cam, _, _ = rt.camera_default(W, H)
         rgba, acc = c.render(cam, spp, seed=seed)
-        assert c.stats().kernel == 0   # RT_KERNEL_MEGA
+        st = c.stats()
+        assert st.kernel == 0   # RT_KERNEL_MEGA
+        assert st.kernel_reason == rt.KERNEL_REASON_TABLES_LDS   # the fallback is visible to the caller
     finally:
         c.close()
     oacc, orgba, _ = O.Scene(meshes).render(W, H, spp, seed=seed)

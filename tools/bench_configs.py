@@ -44,6 +44,27 @@ WHITTED_FLOPS = {"C3": 1.446 * (38.26 * 18 + 2.57 * 54), "C1": 2.3078 * (2 * 25 
 JBF_FLOPS_PER_TAP = 97.0
 
 
+def counters_for(kname, W, H, spp, mode, passes):
+    """The PMC summary of a rocprofv3 pass of THIS build (sha-256 of librt_hip.so) on THIS shape, as bench.py
+    attaches it (profiles/**/pmc_summary.json from profiles/summarize_pmc.py); None without a matching pass."""
+    import glob
+    import hashlib
+    lib = os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so")
+    digest = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None
+    key = f"{kname}:{W}x{H}x{spp}_{mode}_n1_p{passes}"
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "**", "pmc_summary*.json"), recursive=True), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("key") == key and digest is not None and d.get("lib_sha256") == digest:
+            return {"file": os.path.relpath(p, REPO), "kernel_ms_profiled": d.get("kernel_ms"),
+                    **{k: d.get(k) for k in ("valu_issue_frac", "valu_lane_utilization", "valu_wave_insts_per_sample",
+                                              "salu_wave_insts_per_sample", "hbm_bytes_per_sample", "split_read_bytes_per_sample",
+                                              "split_write_bytes_per_sample", "wait_any_frac", "l2_hit_rate")}}
+    return None
+
+
 def flops_per_sample(c):
     if c in WHITTED_FLOPS:
         return WHITTED_FLOPS[c]
@@ -131,10 +152,13 @@ def main():
         fps = flops_per_sample(c)
         roof = None if fps is None else {"bound": "valu", "flops_per_sample": round(fps, 1), "achieved_tflops": round(fps * rate / 1e12, 3),
                                          "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(fps * rate / 1e12 / VALU_PEAK_TFLOPS, 4)}
+        mode = "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")
+        if roof is not None:
+            roof["counters"] = counters_for(rt.KERNEL_NAMES.get(st.kernel, str(st.kernel)), W, H, spp, mode, st.n_passes)
         print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
                           "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "passes": st.n_passes,
                           "prepass_ms": round(st.last_prepass_ms, 3), "path_ms": round(st.last_main_ms, 3), "roofline": roof,
-                          "mode": "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")}), flush=True)
+                          "mode": mode}), flush=True)
         ctx.close()
 
 

@@ -12,6 +12,7 @@
 #   prof                   rocprofv3 trace + PMC passes of the bench command      -> profiles via profiles/run_rocprof.sh
 #   profc5                 the same for C5 at 64 spp                              -> tools/prof_c5.sh
 #   profc5:K=V             the C5 profile with one knob set (e.g. RT_WALK_ORDER=0)
+#   profc3                 trace + PMC passes of C3 (1280x960x64, whitted_kernel)  -> tools/prof_scene.sh
 #   ab:ARGS                tools/ab_libs.py ARGS (comma-separated, e.g. ab:librt_hip.so,librt_hip_x.so,--spp,256)
 #   sweep:ARGS             tools/sweep_env.py ARGS (comma-separated)
 #   sections:LIB:SCENE:SPP[:W:H] wave cycles per kernel section of an RT_SECTIONS build (tools/prof_one.py)
@@ -54,6 +55,8 @@ for step in "$@"; do
       bash profiles/run_rocprof.sh "$TAG" ;;
     profc5)
       bash tools/prof_c5.sh "${TAG}_c5" 64 ;;
+    profc3)
+      bash tools/prof_scene.sh "${TAG}_c3" --scene c3 --width 1280 --height 960 --spp 64 ;;
     profc5:*)
       # the same under one knob (K=V), e.g. profc5:RT_WALK_ORDER=0 -> gpurun_out/prof_TAG_c5_RT_WALK_ORDER0
       kv=${step#profc5:}

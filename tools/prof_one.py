@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--sections", action="store_true", help="print the wave-cycle split of an RT_SECTIONS build")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3"])
     ap.add_argument("--hist", action="store_true", help="print the candidate histograms of an RT_SECTIONS=3 build")
     ap.add_argument("--reps", type=int, default=1, help="measured renders after the warm-up")
     args = ap.parse_args()
@@ -32,15 +32,21 @@ def main():
     spec.loader.exec_module(rt)
     rt.LIB_PATH = os.path.join(PKG, args.lib)
     c = rt.Context(0)
-    if args.scene == "c5":
+    kw = dict(exact=not args.fast)
+    if args.scene in ("c5", "c3"):
         import numpy as np
-        c.upload(rt.Scene.cornell_c5(np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"]))
+        bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
+    if args.scene == "c5":
+        c.upload(rt.Scene.cornell_c5(bvh["raw_bunny"]))
+    elif args.scene == "c3":   # the BVH Ray Tracer's bunny + teapot, Whitted shading (BV/Renderer.cpp:121-233)
+        c.upload(rt.Scene.bvh_tracer(bvh["raw_bunny"], bvh["raw_teapot"]))
+        kw = dict(whitted=True)
     else:
         c.upload(rt.Scene.cornell())
     c.resize(args.width, args.height)
-    cam, _, _ = rt.camera_default(args.width, args.height)
+    cam = rt.camera_bvh_tracer(args.width, args.height) if args.scene == "c3" else rt.camera_default(args.width, args.height)[0]
     for _ in range(1 + args.reps):
-        c.render(cam, args.spp, fetch=False, exact=not args.fast)
+        c.render(cam, args.spp, fetch=False, **kw)
     st = c.stats()
     print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
     if args.sections:
