@@ -739,6 +739,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         const float pdf = 1.0f / (2.0f * 3.141592653589793f);
         P.y_pdf = 1.0f / pdf;
         P.y_rr = p->rr > 0.0f ? 1.0f / p->rr : 0.0f;
+        P.rr_fast = (p->rr >= 0x1p-20f && p->rr < 1.0f) ? 1u : 0u;
         P.lpdf = 1.0f / c->hdr.light_area;
         P.y_lpdf = 1.0f / P.lpdf;
         P.y_w = 1.0f / (float)c->W; P.y_h = 1.0f / (float)c->H;

@@ -138,9 +138,11 @@ struct VertexRng {
 
 // one fold level from the ring: (direct term, cosine) and material -- with ring_pack the material is
 // the three sign bits of the direct term (one 16-byte load instead of two)
-__device__ __forceinline__ void ring_load(const CKParams& Q, size_t at, float4& e, int& m)
+// (the load and the unpacking are separate steps, so that a drain step issues all its ring loads before it waits
+// for the first: with the ring_pack branch inside one load-and-unpack call the compiler waited on each load
+// before issuing the next)
+__device__ __forceinline__ void ring_unpack(const CKParams& Q, size_t at, float4& e, int& m)
 {
-    e = Q.stack_ld[at];
     if (Q.ring_pack) {
         const uint32_t x = __float_as_uint(e.x), y = __float_as_uint(e.y), z = __float_as_uint(e.z);
         m = (int)((x >> 31) | ((y >> 30) & 2u) | ((z >> 29) & 4u));
@@ -252,6 +254,11 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_PEND_FOLD
 #define RT_PEND_FOLD 1
 #endif
+// the fold's two divisions (/PDF, /RR) by one wave-uniform range test and Markstein's correction for the three
+// components (rt_device.h div2_core), instead of div_fast's per-component compare pairs and exec-mask branches
+#ifndef RT_FOLD_DIV2
+#define RT_FOLD_DIV2 1
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -361,17 +368,28 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         const uint32_t R = Q.stack_depth;
         float4 e[N];
         int m[N];
+        uint32_t at[N];
 #pragma unroll
         for (uint32_t j = 0; j < N; ++j) {
             const uint32_t pj = pos >= j ? pos - j : pos + R - j;
-            ring_load(Q, RING_AT(j < dleft ? pj : pos), e[j], m[j]);
+            at[j] = RING_AT(j < dleft ? pj : pos);
+            e[j] = Q.stack_ld[at[j]];
         }
+#pragma unroll
+        for (uint32_t j = 0; j < N; ++j) ring_unpack(Q, at[j], e[j], m[j]);
 #pragma unroll
         for (uint32_t j = 0; j < N; ++j) {
             if (j < dleft) {
                 const float4 mb2 = S.mats[2 * m[j]];
                 const V3 f = (e[j].w >= 0.0f) ? V3{mb2.x, mb2.y, mb2.z} : V3{0.0f, 0.0f, 0.0f};
-                L = add(V3{e[j].x, e[j].y, e[j].z}, vdiv(vdiv(muls(mul(L, f), e[j].w), PDF, Q.y_pdf), Q.rr, Q.y_rr));
+                const V3 x = muls(mul(L, f), e[j].w);
+                V3 q;
+                // both divisions on Markstein's exact path when every lane's numerator is in range (rt_device.h
+                // div2_fast_range; the host sets rr_fast when RR lies in [2^-20, 1)): one wave-uniform test
+                // instead of a compare pair and an exec-mask branch per component and division
+                if (!IEEE_DIV && RT_FOLD_DIV2 && Q.rr_fast && __all(div2_fast_range(x))) q = div2_core(x, PDF, Q.y_pdf, Q.rr, Q.y_rr);
+                else q = vdiv(vdiv(x, PDF, Q.y_pdf), Q.rr, Q.y_rr);
+                L = add(V3{e[j].x, e[j].y, e[j].z}, q);
             }
         }
         const uint32_t n = dleft < N ? dleft : N;

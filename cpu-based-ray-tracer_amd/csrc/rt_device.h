@@ -82,6 +82,32 @@ __device__ __forceinline__ float div_fast(float x, float d, float y)
 
 __device__ __forceinline__ V3 divs_fast(V3 a, float d, float y) { return V3{div_fast(a.x, d, y), div_fast(a.y, d, y), div_fast(a.z, d, y)}; }
 
+// Every component of a in [2^-97, 2^97) or zero: (a / d1) / d2 then takes div_fast's exact path in both divisions
+// for divisors d1, d2 in [2^-20, 1] (|a / d1| <= |a| * 2^20 and >= |a| stay inside [2^-100, 2^100) when
+// 2^-97 <= |a| < 2^77; the fold's divisors are PDF = 1/(2 pi) and the roulette probability, so the bound used
+// below is the tighter [2^-97, 2^77)).  One test per vector instead of two compares and an exec-mask branch per
+// component and division.  Zero: the unsigned (bits - 1) of |a| wraps to the top.
+__device__ __forceinline__ bool div2_fast_range(V3 a)
+{
+    const uint32_t bx = __float_as_uint(a.x) & 0x7FFFFFFFu, by = __float_as_uint(a.y) & 0x7FFFFFFFu, bz = __float_as_uint(a.z) & 0x7FFFFFFFu;
+    const uint32_t lo = __builtin_elementwise_min(__builtin_elementwise_min(bx - 1u, by - 1u), bz - 1u);
+    const uint32_t hi = __builtin_elementwise_max(__builtin_elementwise_max(bx, by), bz);
+    return lo >= 0x0F000000u - 1u && hi < 0x66000000u;   // bits(2^-97) = 0x0F000000, bits(2^77) = 0x66000000
+}
+// (a / d1) / d2 by Markstein's correction in both divisions, for a inside div2_fast_range and d1, d2 in [2^-20, 1]
+// (y1 = RN(1/d1), y2 = RN(1/d2)); a zero component keeps its signed-zero quotient x * y, as div_fast does
+__device__ __forceinline__ float div2_core1(float x, float d1, float y1, float d2, float y2)
+{
+    const float q1 = x * y1;
+    const float a1 = x == 0.0f ? q1 : __builtin_fmaf(__builtin_fmaf(-q1, d1, x), y1, q1);
+    const float q2 = a1 * y2;
+    return a1 == 0.0f ? q2 : __builtin_fmaf(__builtin_fmaf(-q2, d2, a1), y2, q2);
+}
+__device__ __forceinline__ V3 div2_core(V3 a, float d1, float y1, float d2, float y2)
+{
+    return V3{div2_core1(a.x, d1, y1, d2, y2), div2_core1(a.y, d1, y1, d2, y2), div2_core1(a.z, d1, y1, d2, y2)};
+}
+
 // glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
 __device__ __forceinline__ V3 glm_normalize(V3 v) { float is = rcp_f32(__builtin_sqrtf(dot(v, v))); return muls(v, is); }
 __device__ __forceinline__ float glm_length(V3 v) { return __builtin_sqrtf(dot(v, v)); }

@@ -41,6 +41,7 @@ struct KParams {
     // correctly rounded reciprocals of the uniform divisors (host IEEE divisions) for rt_device.h div_fast:
     // 1/PDF (PDF = 1/(2*PI), MC/WhittedMaterial.h:44-56), 1/rr, lpdf = 1/light_area and 1/lpdf, 1/W, 1/H
     float y_pdf, y_rr, lpdf, y_lpdf, y_w, y_h;
+    uint32_t rr_fast;   // rr in [2^-20, 1): the fold's division by rr may take Markstein's path (rt_device.h div2_core)
     // pixels of this device: row bands of `band` rows dealt round-robin over `nranks`
     uint32_t band, rank, nranks, n_local_rows;
     uint32_t tiles_x; uint32_t n_items;

@@ -2,12 +2,16 @@
 5.1), on the CPU.
 
 A split scene's walked subtree is stored in 8 pre-orders, one per ray-direction octant, each visiting the
-nearer child first.  The kernel walks them stacklessly (hit: next node, miss or leaf: the node's skip
-pointer) and ends when the pointer reads n_nodes.  The GPU tests check the images bitwise
-(test_c5.py, test_split_adversarial.py); these check the tables themselves: every ordering holds the
-subtree's nodes exactly once, its skip pointers describe a well-formed pre-order that ends at n_nodes, and a
+nearer child first -- of the reference's subtree itself (RT_WALK_TREE=0) or (default) of a binned-SAH tree
+built over the subtree's leaves (the same leaf boxes and triangles, internal boxes their unions).  The kernel
+walks them stacklessly (hit: next node, miss or leaf: the node's skip pointer) and ends when the pointer reads
+n_nodes.  The GPU tests check the images bitwise (test_c5.py, test_split_adversarial.py); these check the
+tables themselves: every ordering holds the subtree's leaves exactly once (and, for the reference's tree, its
+internal nodes too), every internal box contains its children's (so a leaf box's own slab test decides
+whether the walk reaches it), its skip pointers describe a well-formed pre-order that ends at n_nodes, and a
 walk under any box predicate reaches the same leaves as the reference's DFS walk of the subtree -- the
-kernel keeps the closest hit by (min t, max DFS triangle), so the visit order does not change its result."""
+kernel keeps the closest hit by (min t, max DFS triangle), so neither the tree nor the visit order changes
+its result."""
 import numpy as np
 import pytest
 
@@ -58,7 +62,7 @@ def slab(o, d):
     return hit
 
 
-def check_orders(sc, n_rays, seed):
+def check_orders(sc, n_rays, seed, same_tree):
     info = sc.info()
     r, e, NN = info.split_root, info.split_end, info.n_nodes
     assert r > 0
@@ -66,13 +70,16 @@ def check_orders(sc, n_rays, seed):
     Wall = sc.walk_orders()
     M = e - r
     assert Wall.shape == (8, M, 8)
-    ref_rows = np.sort(np.concatenate([boxes[r:e], tri[r:e, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
+    rows_of = lambda b, t, m: np.sort(np.concatenate([b[m], t[m, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
+    sub_tri = tri[r:e]
+    ref_rows = rows_of(boxes[r:e], sub_tri, np.ones(len(sub_tri), bool) if same_tree else sub_tri >= 0)
     rng = np.random.default_rng(seed)
     lo, hi = boxes[r, :3].astype(np.float64), boxes[r, 3:].astype(np.float64)
     for oct_ in range(8):
         bx, sk, tr = copy_fields(Wall[oct_])
-        # the same nodes (box, triangle), each once
-        rows = np.sort(np.concatenate([bx, tr[:, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
+        # the same leaves (box, triangle), each once; for the reference's tree every node
+        assert len(bx) == M
+        rows = rows_of(bx, tr, np.ones(M, bool) if same_tree else tr >= 0)
         assert np.array_equal(rows, ref_rows)
         # a well-formed pre-order: a leaf's skip is the next row, an internal node's first child is the next
         # row and its second child's skip equals its own; every pointer stays in [r + 1, e) or reads NN
@@ -86,11 +93,15 @@ def check_orders(sc, n_rays, seed):
         assert np.all(right < sk_in[inner])
         assert np.all(sk_in[right - r] == sk_in[inner])
         assert sk[0] == NN   # the walk ends at n_nodes
+        # every internal box contains both children's boxes (float compares: exact containment)
+        first, second = inner + 1, right - r
+        for ch in (first, second):
+            assert np.all(bx[inner, :3] <= bx[ch, :3]) and np.all(bx[inner, 3:] >= bx[ch, 3:])
         # everything hit: all M nodes in row order
         leaves, visits = walk(bx, sk, tr, r, NN, r, lambda b: True)
         assert visits == M and len(leaves) == int(leaf.sum())
-    # rays through the subtree's box: the ordering of the ray's octant reaches the DFS walk's leaves, with
-    # the same boxes tested
+    # rays through the subtree's box: the ordering of the ray's octant reaches the DFS walk's leaves (with the
+    # same boxes tested when the tree is the reference's)
     for _ in range(n_rays):
         tgt = lo + (hi - lo) * rng.random(3)
         o = tgt + rng.normal(size=3) * (hi - lo).max()
@@ -101,18 +112,24 @@ def check_orders(sc, n_rays, seed):
         ref_leaves, ref_visits = walk(boxes, skip, tri, r, e, 0, hit)
         bx, sk, tr = copy_fields(Wall[oct_])
         leaves, visits = walk(bx, sk, tr, r, NN, r, hit)
-        assert sorted(leaves) == sorted(ref_leaves) and visits == ref_visits
+        assert sorted(leaves) == sorted(ref_leaves)
+        if same_tree:
+            assert visits == ref_visits
 
 
-def test_walk_orders_of_the_adversarial_split_scene():
+@pytest.mark.parametrize("walk_tree", ["0", "1"], ids=["reference-subtree", "sah-tree"])
+def test_walk_orders_of_the_adversarial_split_scene(walk_tree, monkeypatch):
+    monkeypatch.setenv("RT_WALK_TREE", walk_tree)
     sc = SA.A.build_rt(SA.split_scene())
-    check_orders(sc, n_rays=300, seed=1)
+    check_orders(sc, n_rays=300, seed=1, same_tree=walk_tree == "0")
 
 
-def test_walk_orders_of_c5():
+@pytest.mark.parametrize("walk_tree", ["0", "1"], ids=["reference-subtree", "sah-tree"])
+def test_walk_orders_of_c5(walk_tree, monkeypatch):
+    monkeypatch.setenv("RT_WALK_TREE", walk_tree)
     bvh = np.load(SA.A.__file__.replace("test_skip_adversarial.py", "golden/bvh_scene.npz"))
     sc = rt.Scene.cornell_c5(bvh["raw_bunny"])
-    check_orders(sc, n_rays=40, seed=2)
+    check_orders(sc, n_rays=40, seed=2, same_tree=walk_tree == "0")
 
 
 def test_small_scenes_have_no_walk_orders():

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of context-level knobs read from the environment at rt_create (RT_THRESH, RT_STEPS,
-RT_CHUNKS, RT_ITEMS_PER_LANE, RT_MIN_PX_PER_LANE) in ONE process, interleaved rounds, optionally on a
+RT_CHUNKS, RT_ITEMS_PER_LANE, RT_MIN_PX_PER_LANE) and at the scene build (RT_WALK_TREE) in ONE process, interleaved rounds, optionally on a
 row band of an N-rank frame (--rank/--nranks) to see multi-GPU per-rank behaviour on one GPU.
 
     python tools/sweep_env.py --set "RT_CHUNKS=1" --set "RT_CHUNKS=2" --nranks 8
@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from _rt import rt  # noqa: E402
 
-KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_WALK_MASK", "RT_BVH_PREPASS", "RT_PRE_DEFER")
+KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_WALK_MASK", "RT_BVH_PREPASS", "RT_PRE_DEFER", "RT_WALK_TREE")
 
 
 def main():
@@ -37,10 +37,7 @@ def main():
     if args.lib:
         rt.LIB_PATH = os.path.join(REPO, "cpu-based-ray-tracer_amd", args.lib)
     W, H, spp = args.width, args.height, args.spp
-    if args.scene == "c5":
-        scene = rt.Scene.cornell_c5(np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"])
-    else:
-        scene = rt.Scene.cornell()
+    bunny = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"] if args.scene == "c5" else None
     cam, _, _ = rt.camera_default(W, H)
     variants = args.set or [""]
     ctxs = []
@@ -50,6 +47,8 @@ def main():
         for a in v.replace(",", " ").split():
             k, val = a.split("=")
             os.environ[k] = val
+        # the scene is built under the variant's knobs too (RT_WALK_TREE is read by the scene build)
+        scene = rt.Scene.cornell_c5(bunny) if args.scene == "c5" else rt.Scene.cornell()
         c = rt.Context(0)
         c.upload(scene)
         c.resize(W, H, 8, args.rank, args.nranks)
