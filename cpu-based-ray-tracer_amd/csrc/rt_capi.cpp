@@ -98,6 +98,8 @@ struct rt_ctx {
     uint64_t lbuf_budget = 96ull << 30;   // bytes of parked samples (+ camera records) per launch; C4 needs 59 GB of 288
     bool lbuf_budget_env = false;         // RT_LBUF_BUDGET_MB given: else min(96 GB, 3/4 of free memory) per render
     float* d_lbuf = nullptr;
+    uint32_t* d_sky = nullptr;    // pre-pass sky bits (KParams::sky_bits)
+    size_t sky_words_alloc = 0;
     size_t lbuf_floats = 0;
     // the vertex kernel's camera pre-pass: surface-hit records, per-segment counts, the non-empty segments
     float4* d_crec = nullptr;
@@ -108,6 +110,7 @@ struct rt_ctx {
     size_t tile_words = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
+    bool sky_bits = true;   // the pre-pass's camera-ray misses as bits, not parked samples (RT_SKY_BITS=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
@@ -435,6 +438,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_STEPS")) c->steps = c->vsteps = c->ssteps = std::max<uint32_t>(1, (uint32_t)std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = rt_knob("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_SKY_BITS")) c->sky_bits = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
@@ -510,7 +514,7 @@ void rt_destroy(rt_ctx* c)
     dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
-    dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf);
+    dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf); dfree(c->d_sky);
     dfree(c->d_crec); dfree(c->d_ccount); dfree(c->d_seg_list); dfree(c->d_tile_boxes);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev3) (void)hipEventDestroy(c->ev3);
@@ -740,6 +744,8 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         P.y_pdf = 1.0f / pdf;
         P.y_rr = p->rr > 0.0f ? 1.0f / p->rr : 0.0f;
         P.rr_fast = (p->rr >= 0x1p-20f && p->rr < 1.0f) ? 1u : 0u;
+        P.lpdf_fast = (P.lpdf >= 0x1p-20f && P.lpdf < 0x1p20f) ? 1u : 0u;
+        P.wh_fast = (c->W >= 1u && c->W < (1u << 20) && c->H >= 1u && c->H < (1u << 20)) ? 1u : 0u;
         P.lpdf = 1.0f / c->hdr.light_area;
         P.y_lpdf = 1.0f / P.lpdf;
         P.y_w = 1.0f / (float)c->W; P.y_h = 1.0f / (float)c->H;
@@ -975,6 +981,21 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                         c->tile_words = 0;
                         HIPC(c, hipMalloc((void**)&c->d_tile_boxes, (size_t)Q.n_tiles * 8));
                         c->tile_words = Q.n_tiles;
+                    }
+                    // sky bits: with segments of >= 32 frames (a segment then owns whole 32-frame words) the pre-pass
+                    // sets a bit for a camera-ray miss instead of parking the sky's radiance (RT_SKY_BITS=0: park it)
+                    Q.sky_bits = nullptr; Q.sky_words = 0;
+                    if (c->sky_bits && park_all && Q.seg_frames >= 32u) {
+                        const uint32_t sw = (nf + 31u) / 32u;
+                        const size_t need = (size_t)sw * px_local;
+                        if (need > c->sky_words_alloc) {
+                            HIPC(c, hipStreamSynchronize(c->stream));
+                            dfree(c->d_sky);
+                            c->sky_words_alloc = 0;
+                            HIPC(c, hipMalloc((void**)&c->d_sky, need * sizeof(uint32_t)));
+                            c->sky_words_alloc = need;
+                        }
+                        Q.sky_bits = c->d_sky; Q.sky_words = sw;
                     }
                     Q.crec = c->d_crec; Q.ccount = c->d_ccount; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
                     Q.tile_boxes = c->d_tile_boxes;

@@ -259,6 +259,11 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_FOLD_DIV2
 #define RT_FOLD_DIV2 1
 #endif
+// the same in the BVH variant's fold (whose other divisions keep the IEEE sequences, RT_BVH_DIV_FAST): C5
+// 3840x2160x64 5842 -> 5973 Msamples/s, bitwise (the per-component div_fast had cost this variant registers)
+#ifndef RT_BVH_FOLD_DIV2
+#define RT_BVH_FOLD_DIV2 1
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -387,7 +392,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 // both divisions on Markstein's exact path when every lane's numerator is in range (rt_device.h
                 // div2_fast_range; the host sets rr_fast when RR lies in [2^-20, 1)): one wave-uniform test
                 // instead of a compare pair and an exec-mask branch per component and division
-                if (!IEEE_DIV && RT_FOLD_DIV2 && Q.rr_fast && __all(div2_fast_range(x))) q = div2_core(x, PDF, Q.y_pdf, Q.rr, Q.y_rr);
+                if ((!IEEE_DIV || RT_BVH_FOLD_DIV2) && RT_FOLD_DIV2 && Q.rr_fast && __all(div2_fast_range(x))) q = div2_core(x, PDF, Q.y_pdf, Q.rr, Q.y_rr);
                 else q = vdiv(vdiv(x, PDF, Q.y_pdf), Q.rr, Q.y_rr);
                 L = add(V3{e[j].x, e[j].y, e[j].z}, q);
             }
@@ -891,9 +896,15 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
                     const float4 mb = S.mats[2 * mat];
                     const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
-                    const V3 ldu = vdiv(vdiv(muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2), sd2,
-                                             IEEE_DIV ? 0.0f : rcp_f32(sd2)),
-                                        Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
+                    const V3 X = muls(muls(mul(V3{Q.light_emission[0], Q.light_emission[1], Q.light_emission[2]}, f), sc1), sc2);
+                    V3 ldu;
+                    // (X / dist^2) / light PDF: both on Markstein's exact path when every lane's numerator lies in
+                    // [2^-77, 2^77) (or is zero) and its dist^2 in [2^-20, 2^20) (the quotient then stays inside
+                    // [2^-97, 2^97)), one wave-uniform test (rt_device.h div2_fast_range), as the fold's
+                    if (!IEEE_DIV && RT_FOLD_DIV2 && Q.lpdf_fast && __all(div2_fast_range<0x19000000u, 0x66000000u>(X) && sd2 >= 0x1p-20f && sd2 < 0x1p20f))
+                        ldu = div2_core(X, sd2, rcp_f32_mid(sd2), Q.lpdf, Q.y_lpdf);
+                    else
+                        ldu = vdiv(vdiv(X, sd2, IEEE_DIV ? 0.0f : rcp_f32(sd2)), Q.lpdf, Q.y_lpdf);   // Q.lpdf = 1.0f / light_area
                     st3(VS_LD, ldu);
                     dB = wl;
                     // a zero unoccluded term (the light behind the surface: f = 0) makes the verdict pick
@@ -1538,6 +1549,7 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
     const bool split = BVH && P.split_root != 0u;
     const uint64_t boxes = (BVH && !split) ? ~0ull : P.tile_boxes[tile];
     uint32_t cnt = 0;
+    uint64_t skym = 0;   // the segment's camera-ray misses (P.sky_bits): bit j = frame f0 + j
     for (uint32_t j = 0; j < nf; ++j) {
         const uint32_t fidx = f0 + j, frame = P.first_frame + fidx;
         // the camera ray: the two camera draws (dims 0, 1 of the sample's stream), jitter, NDC,
@@ -1545,13 +1557,28 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
         uint32_t ow[4];
         philox4x32_10(pix, frame, 0u, 0u, (uint32_t)P.seed, (uint32_t)(P.seed >> 32), ow);
         const float ux = (float)ow[0] / 4294967296.0f, uy = (float)ow[1] / 4294967296.0f;
-        float cx = div_fast((float)lx + ux, (float)P.W, P.y_w);
-        float cy = div_fast((float)y + uy, (float)P.H, P.y_h);
+        // the divisions by Markstein's correction: (x + u) / W and (y + u) / H have numerators 0 or in [2^-32, 2^21)
+        // (wh_fast: W and H below 2^20, a host flag), xyz / w when a wave-uniform test finds every operand in range
+        float cx, cy;
+        if (RT_FOLD_DIV2 && P.wh_fast) {
+            cx = div1_core((float)lx + ux, (float)P.W, P.y_w);
+            cy = div1_core((float)y + uy, (float)P.H, P.y_h);
+        } else {
+            cx = div_fast((float)lx + ux, (float)P.W, P.y_w);
+            cy = div_fast((float)y + uy, (float)P.H, P.y_h);
+        }
         cx = cx * 2.0f - 1.0f;
         cy = cy * 2.0f - 1.0f;
         float tg[4];
         mat4_mul(P.iproj, cx, cy, 1.0f, 1.0f, tg);
-        const V3 dv = glm_normalize(divs_fast(V3{tg[0], tg[1], tg[2]}, tg[3], rcp_f32(tg[3])));
+        const V3 txyz{tg[0], tg[1], tg[2]};
+        V3 dq;
+        const float aw = __builtin_fabsf(tg[3]);
+        if (RT_FOLD_DIV2 && __all(div2_fast_range<kBits2m100, kBits2p100>(txyz) && aw >= 0x1p-20f && aw < 0x1p20f))
+            dq = div1_core(txyz, tg[3], rcp_f32_mid(tg[3]));
+        else
+            dq = divs_fast(txyz, tg[3], rcp_f32(tg[3]));
+        const V3 dv = glm_normalize(dq);
         float wd[4];
         mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
         const V3 d = w_normalize(V3{wd[0], wd[1], wd[2]});
@@ -1655,11 +1682,21 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
                     rec = make_float4(loc.x, loc.y, loc.z, __uint_as_float((uint32_t)tri | (lane << 19) | (j << 25) | (flip ? 0x80000000u : 0u)));
                 }
             }
-            if (!surface) park_sample(P, L, local, fidx);
+            if (!surface) {
+                if (P.sky_bits != nullptr && tri < 0) skym |= 1ull << j;   // the night sky: a bit, not a parked sample
+                else park_sample(P, L, local, fidx);
+            }
         }
         const uint64_t hits = __ballot(surface);
         if (surface) out[cnt + (uint32_t)__popcll(hits & ((1ull << lane) - 1ull))] = rec;
         cnt += (uint32_t)__popcll(hits);
+    }
+    if (P.sky_bits != nullptr && valid) {
+        // the segment's whole 32-frame words (segments of >= 32 frames start on a word: rt_capi.cpp), word-major
+        const size_t px = (size_t)P.n_local_rows * P.W;
+        const uint32_t w0 = f0 >> 5;
+        P.sky_bits[(size_t)w0 * px + local] = (uint32_t)skym;
+        if (nf > 32u) P.sky_bits[(size_t)(w0 + 1u) * px + local] = (uint32_t)(skym >> 32);
     }
     if (lane == 0) {
         P.ccount[sg] = cnt;

@@ -87,12 +87,20 @@ __device__ __forceinline__ V3 divs_fast(V3 a, float d, float y) { return V3{div_
 // 2^-97 <= |a| < 2^77; the fold's divisors are PDF = 1/(2 pi) and the roulette probability, so the bound used
 // below is the tighter [2^-97, 2^77)).  One test per vector instead of two compares and an exec-mask branch per
 // component and division.  Zero: the unsigned (bits - 1) of |a| wraps to the top.
+// (LO, HI: the bit patterns of the bounds; the defaults are bits(2^-97) = 0x0F000000 and bits(2^77) = 0x66000000)
+template <uint32_t LO = 0x0F000000u, uint32_t HI = 0x66000000u>
 __device__ __forceinline__ bool div2_fast_range(V3 a)
 {
     const uint32_t bx = __float_as_uint(a.x) & 0x7FFFFFFFu, by = __float_as_uint(a.y) & 0x7FFFFFFFu, bz = __float_as_uint(a.z) & 0x7FFFFFFFu;
     const uint32_t lo = __builtin_elementwise_min(__builtin_elementwise_min(bx - 1u, by - 1u), bz - 1u);
     const uint32_t hi = __builtin_elementwise_max(__builtin_elementwise_max(bx, by), bz);
-    return lo >= 0x0F000000u - 1u && hi < 0x66000000u;   // bits(2^-97) = 0x0F000000, bits(2^77) = 0x66000000
+    return lo >= LO - 1u && hi < HI;
+}
+// the correctly rounded 1 / d for d in [2^-20, 2^20) (rcp_f32's Newton step without its range branch)
+__device__ __forceinline__ float rcp_f32_mid(float d)
+{
+    const float r = __builtin_amdgcn_rcpf(d);
+    return __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
 }
 // (a / d1) / d2 by Markstein's correction in both divisions, for a inside div2_fast_range and d1, d2 in [2^-20, 1]
 // (y1 = RN(1/d1), y2 = RN(1/d2)); a zero component keeps its signed-zero quotient x * y, as div_fast does
@@ -107,6 +115,15 @@ __device__ __forceinline__ V3 div2_core(V3 a, float d1, float y1, float d2, floa
 {
     return V3{div2_core1(a.x, d1, y1, d2, y2), div2_core1(a.y, d1, y1, d2, y2), div2_core1(a.z, d1, y1, d2, y2)};
 }
+// one division x / d on Markstein's path, for x == 0 or 2^-100 <= |x| < 2^100 and d in [2^-20, 2^20)
+// (the caller tests the ranges once, for a wave: div2_fast_range<bits(2^-100), bits(2^100)> for a vector)
+__device__ __forceinline__ float div1_core(float x, float d, float y)
+{
+    const float q = x * y;
+    return x == 0.0f ? q : __builtin_fmaf(__builtin_fmaf(-q, d, x), y, q);
+}
+__device__ __forceinline__ V3 div1_core(V3 a, float d, float y) { return V3{div1_core(a.x, d, y), div1_core(a.y, d, y), div1_core(a.z, d, y)}; }
+constexpr uint32_t kBits2m100 = 0x0D800000u, kBits2p100 = 0x71800000u;   // bits(2^-100), bits(2^100)
 
 // glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
 __device__ __forceinline__ V3 glm_normalize(V3 v) { float is = rcp_f32(__builtin_sqrtf(dot(v, v))); return muls(v, is); }

@@ -42,6 +42,8 @@ struct KParams {
     // 1/PDF (PDF = 1/(2*PI), MC/WhittedMaterial.h:44-56), 1/rr, lpdf = 1/light_area and 1/lpdf, 1/W, 1/H
     float y_pdf, y_rr, lpdf, y_lpdf, y_w, y_h;
     uint32_t rr_fast;   // rr in [2^-20, 1): the fold's division by rr may take Markstein's path (rt_device.h div2_core)
+    uint32_t lpdf_fast; // lpdf in [2^-20, 2^20): the direct term's division by the light PDF likewise
+    uint32_t wh_fast;   // W and H below 2^20: the camera's divisions by W and H likewise
     // pixels of this device: row bands of `band` rows dealt round-robin over `nranks`
     uint32_t band, rank, nranks, n_local_rows;
     uint32_t tiles_x; uint32_t n_items;
@@ -54,6 +56,10 @@ struct KParams {
     // frame-major: [frame - chunk_frames][local]) for the in-order sum of finalize_chunks_kernel
     uint32_t n_chunks, chunk_frames, items_per_chunk;
     float* lbuf; size_t lbuf_stride;
+    // camera-ray misses of the pre-pass (the night sky, MC/Renderer.cpp:145) as bits instead of parked samples: bit
+    // (fidx % 32) of word [fidx / 32][local] (null: every sample is parked); finalize_chunks_kernel adds the sky's
+    // radiance for a set bit and reads the parked slot only for the others
+    uint32_t* sky_bits; uint32_t sky_words;
     uint32_t park_all;              // every frame is parked (the vertex kernel): finalize accumulates all of them
     uint32_t lbuf_pixel_major;      // park_all: a pixel's 4-frame blocks are contiguous ([pixel][block]) instead of
                                     // [block][pixel] (lbuf_stride pixels apart)

@@ -623,16 +623,27 @@ __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_
     // the accumulator otherwise; else chunk 0 has accumulated in place and the later chunks are parked
     float4 acc = (P.park_all && P.first_frame == 1u) ? make_float4(0.f, 0.f, 0.f, 0.f) : P.accum[i];
     const uint32_t nfp = P.park_all ? P.n_frames : P.n_frames - P.chunk_frames;
+    // the pre-pass's sky bits (KParams::sky_bits): a camera-ray miss adds the night sky's radiance, which the pre-pass
+    // would have parked (cast_path, MC/Renderer.cpp:145); a 4-frame block of misses is not read at all
+    const float SKY_R = 12 / 255.0f, SKY_G = 20 / 255.0f, SKY_B = 69 / 255.0f;
+    uint32_t skyw = 0;
     for (uint32_t b = 0; b * 4u < nfp; ++b) {
-        const size_t bi = (P.park_all && P.lbuf_pixel_major) ? (size_t)i * ((nfp + 3u) >> 2) + b : (size_t)b * P.lbuf_stride + i;
-        const float4* blk = reinterpret_cast<const float4*>(P.lbuf + bi * 12u);
-        const float4 q0 = blk[0], q1 = blk[1], q2 = blk[2];
-        const float v[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+        if (P.sky_bits != nullptr && (b & 7u) == 0u) skyw = P.sky_bits[(size_t)(b >> 3) * P.lbuf_stride + i];
+        const uint32_t sky4 = P.sky_bits != nullptr ? (skyw >> (4u * (b & 7u))) & 0xFu : 0u;
         const uint32_t n = min(4u, nfp - b * 4u);
+        float v[12];
+        if (sky4 != ((1u << n) - 1u)) {
+            const size_t bi = (P.park_all && P.lbuf_pixel_major) ? (size_t)i * ((nfp + 3u) >> 2) + b : (size_t)b * P.lbuf_stride + i;
+            const float4* blk = reinterpret_cast<const float4*>(P.lbuf + bi * 12u);
+            const float4 q0 = blk[0], q1 = blk[1], q2 = blk[2];
+            v[0] = q0.x; v[1] = q0.y; v[2] = q0.z; v[3] = q0.w; v[4] = q1.x; v[5] = q1.y;
+            v[6] = q1.z; v[7] = q1.w; v[8] = q2.x; v[9] = q2.y; v[10] = q2.z; v[11] = q2.w;
+        }
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
             if (j < n) {
-                acc.x = acc.x + v[3 * j]; acc.y = acc.y + v[3 * j + 1]; acc.z = acc.z + v[3 * j + 2];
+                const bool sky = (sky4 >> j) & 1u;
+                acc.x = acc.x + (sky ? SKY_R : v[3 * j]); acc.y = acc.y + (sky ? SKY_G : v[3 * j + 1]); acc.z = acc.z + (sky ? SKY_B : v[3 * j + 2]);
                 acc.w = acc.w + 1.0f;
             }
         }
