@@ -60,7 +60,7 @@ class GroupStats(C.Structure):
     _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
 
 
-_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders"}   # may be absent from an older A/B build
+_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders", "rt_scene_whitted_orders"}   # may be absent from an older A/B build
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 # rt_stats.kernel_reason (include/rt_capi.h RT_KERNEL_REASON_*)
@@ -127,6 +127,7 @@ def lib():
         "rt_upload_scene_gpu_bvh": (i32, [vp, vp, fp]),
         "rt_scene_lbvh_host": (i32, [vp, fp, fp]),
         "rt_scene_walk_orders": (i32, [vp, fp, C.POINTER(C.c_uint64)]),
+        "rt_scene_whitted_orders": (i32, [vp, fp, C.POINTER(C.c_uint64)]),
         "rt_debug_scene_arrays": (i32, [vp, fp, u32, fp, u32]),
         "rt_resize": (i32, [vp, u32, u32, u32, u32, u32]),
         "rt_local_rows": (u32, [vp]),
@@ -300,15 +301,18 @@ class Scene:
         self._check(lib().rt_scene_lbvh_host(self.h, _fp(nodes), _fp(tris)), "rt_scene_lbvh_host")
         return nodes, tris
 
-    def walk_orders(self):
+    def walk_orders(self, whitted=False):
         """The split subtree's 8 near-first pre-orders (rt_scene_walk_orders): (8, split_end - split_root, 8)
-        float32 in the traversal layout, or None when the scene has no split."""
+        float32 in the traversal layout, or None when the scene has no split; whitted=True: a Whitted scene's
+        whole tree (rt_scene_whitted_orders, (8, n_nodes, 8))."""
+        name = "rt_scene_whitted_orders" if whitted else "rt_scene_walk_orders"
+        fn = getattr(lib(), name)
         n = C.c_uint64(0)
-        self._check(lib().rt_scene_walk_orders(self.h, None, C.byref(n)), "rt_scene_walk_orders")
+        self._check(fn(self.h, None, C.byref(n)), name)
         if n.value == 0:
             return None
         out = np.zeros(n.value, np.float32)
-        self._check(lib().rt_scene_walk_orders(self.h, _fp(out), C.byref(n)), "rt_scene_walk_orders")
+        self._check(fn(self.h, _fp(out), C.byref(n)), name)
         return out.reshape(8, -1, 8)
 
     def export(self):

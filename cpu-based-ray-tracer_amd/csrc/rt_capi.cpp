@@ -36,6 +36,7 @@ struct rt_ctx {
     float4* d_sboxes = nullptr;   // split trace (FlatScene::sboxes): outside leaf boxes
     int32_t* d_stri = nullptr;    // split trace: outside slot -> triangle
     float4* d_wcopies = nullptr;  // split trace: near-first orderings of the walked subtree (FlatScene::wcopies)
+    float4* d_worders = nullptr;  // Whitted scenes: near-first orderings of the whole tree (FlatScene::worders)
     uint32_t split_root = 0, split_end = 0, n_sboxes = 0, n_sleaves = 0;
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
@@ -116,6 +117,7 @@ struct rt_ctx {
     bool lbuf_pm = false;   // diagnostic: the vertex kernel's parked samples pixel-major (RT_LBUF_PIXEL_MAJOR=1; -1 % C4/C5)
     bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
     bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
+    bool wh_order = true;     // Whitted kernel: walk the whole tree's near-first ordering of the ray's octant (RT_WH_ORDER=0: DFS)
     uint32_t walk_mask = 7;   // A/B (RT_WALK_MASK): the ordering a ray walks is its octant & mask (fewer orderings in use)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
@@ -426,6 +428,15 @@ rt_status rt_scene_walk_orders(const rt_scene* s, float* out, uint64_t* n_floats
     return RT_OK;
 }
 
+rt_status rt_scene_whitted_orders(const rt_scene* s, float* out, uint64_t* n_floats)
+{
+    if (!s || !s->built) return RT_ERR_STATE;
+    if (!n_floats) return RT_ERR_INVALID;
+    *n_floats = s->flat.worders.size();
+    if (out && !s->flat.worders.empty()) std::memcpy(out, s->flat.worders.data(), s->flat.worders.size() * sizeof(float));
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ context
 rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
 {
@@ -442,6 +453,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_WH_ORDER")) c->wh_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_MASK")) c->walk_mask = (uint32_t)std::strtoul(e, nullptr, 10) & 7u;
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
@@ -509,7 +521,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies);
+    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_lboxes); dfree(c->d_wmats); dfree(c->d_plights);
     dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
     dfree(c->d_went); dfree(c->d_wtris);
@@ -549,6 +561,8 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
         static const std::vector<float> kNone;
         const bool walks = c->vertex && c->vertex_bvh && c->split && c->walk_order && !c->qbvh && !c->force_walk;
         if ((r = upload(c, c->d_wcopies, walks ? s->flat.wcopies : kNone)) != RT_OK) return r;
+        // (8 x the whole tree's nodes for a Whitted scene: 38 MB at C3)
+        if ((r = upload(c, c->d_worders, c->wh_order ? s->flat.worders : kNone)) != RT_OK) return r;
     }
     c->split_root = s->flat.split_root;
     c->split_end = s->flat.split_end;
@@ -633,7 +647,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     c->d_nodes = d_nodes; c->d_tris = d_tris;
     // the BVH-walking kernels: no leaf-box table, no compact tree
     dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
-    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies);   // the split refers to the host tree's node order
+    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders);   // the split and orderings refer to the host tree's node order
     c->split_root = c->split_end = c->n_sboxes = c->n_sleaves = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
@@ -722,6 +736,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             P.wcopy_mask = c->walk_mask;
         }
     }
+    P.worders = c->d_worders;
     P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
     P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;
     std::memcpy(P.q_origin, c->hdr.q_origin, sizeof P.q_origin);

@@ -264,6 +264,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BVH_FOLD_DIV2
 #define RT_BVH_FOLD_DIV2 1
 #endif
+#ifndef RT_REC_FIRST
+#define RT_REC_FIRST 0
+#endif
+#ifndef RT_WALK_PAIR
+#define RT_WALK_PAIR 0
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -631,13 +637,19 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         // (a path ends at a vertex's service; a camera ray's service is its hit: !PRE, or the BVH variant's camera
         // rays the pre-pass left to it)
         const bool ends = served && ((PRE && !BVH) || pend) && (!cont || triA < 0 || emissive);
+        uint32_t rid = NO_REC;
+        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
+        // RT_REC_FIRST: the record loads are issued before the drain's ring loads, so both latencies overlap and
+        // the drain's parked-sample store comes after them (a load issued after a store waits for it);
+        // otherwise after the drain (the record's registers are then not live across the fold)
+        if constexpr (PRE && RT_REC_FIRST) {
+            rid = take_records(alive && (!in_path || ends));
+            if (rid != NO_REC) rec = kargs4().crec[rid];
+        }
         if (EXACT && __any(dleft != 0u || hasPend)) {
             if (dleft != 0u || hasPend) drain_step(dleft);
         }
-        // (after the drain's ring loads are folded: the record's registers are then not live across them)
-        uint32_t rid = NO_REC;
-        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (PRE) {
+        if constexpr (PRE && !RT_REC_FIRST) {
             rid = take_records(alive && (!in_path || ends));
             if (rid != NO_REC) rec = kargs4().crec[rid];
         }
@@ -1303,16 +1315,33 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         const float4* wn = S.nodes;
                         if (Q.wcopies != nullptr && (decltype(kind)::value || finite3(r.rcp)))
                             wn = Q.wcopies + (((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) & Q.wcopy_mask) * Q.wcopy_stride;
-                        for (uint32_t s = 0; s < steps && ti < tend; ++s) {
-                            const float4 q0 = wn[2 * ti];
-                            const float4 q1 = wn[2 * ti + 1];
+                        auto test_node = [&](const float4 q0, const float4 q1) -> bool {   // true: go on to ti + 1
                             const bool hit = decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
                                                                    : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                             const int tri = f2i(q1.w);
                             ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
                             if (hit && tri >= 0) {
                                 if (parked0 < 0) parked0 = tri;
-                                else { parked1 = tri; break; }
+                                else { parked1 = tri; return false; }
+                            }
+                            return true;
+                        };
+                        if (RT_WALK_PAIR) {
+                            // two nodes per dependent load: node ti and its pre-order successor ti + 1, which the walk
+                            // visits next whenever ti is entered or is a leaf (a leaf's skip is ti + 1); the second
+                            // test is wasted when ti is a missed internal node
+                            for (uint32_t s = 0; s < steps && ti < tend; ++s) {
+                                const uint32_t t0 = ti, t1 = ti + 1u < tend ? ti + 1u : ti;
+                                const float4 q0 = wn[2 * t0], q1 = wn[2 * t0 + 1], q2 = wn[2 * t1], q3 = wn[2 * t1 + 1];
+                                if (!test_node(q0, q1)) break;
+                                if (ti != t0 + 1u || ti >= tend) continue;
+                                if (!test_node(q2, q3)) break;
+                            }
+                        } else {
+                            for (uint32_t s = 0; s < steps && ti < tend; ++s) {
+                                const float4 q0 = wn[2 * ti];
+                                const float4 q1 = wn[2 * ti + 1];
+                                if (!test_node(q0, q1)) break;
                             }
                         }
                     };

@@ -21,6 +21,9 @@ struct KParams {
     // the subtree's near-first orderings (rt_scene.h FlatScene::wcopies; null: off): ordering o's node k at
     // wcopies[2 * k + o * wcopy_stride], k in [split_root, split_end) (the pointer is offset by -2 * split_root)
     const float4* wcopies; uint32_t wcopy_stride, wcopy_mask;   // ordering = octant & wcopy_mask (7; A/B: fewer in use)
+    // Whitted scenes: the whole tree's near-first orderings (FlatScene::worders; null: the DFS walk), ordering
+    // o's node k at worders[2 * (o * n_nodes + k)]
+    const float4* worders;
     // (the BVH variant stages the small tables (mats | lnodes | ltris) in LDS, the split's outside triangles
     //  (3 float4 per slot: a, e1, (e2, bits(triangle))) after them; rt_capi.cpp checks that they fit)
     // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex

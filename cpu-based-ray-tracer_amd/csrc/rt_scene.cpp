@@ -552,6 +552,66 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             }
         }
     }
+    // near-first orderings of the subtree [r, rend) (the whole tree: [0, NN)), one per direction octant (bit 0:
+    // d.x < 0, bit 1: d.y, bit 2: d.z): the same leaves in the pre-order that visits, at every internal node,
+    // first the child whose box centre lies nearer along the axis that separates the two centres most, node k
+    // of ordering o at dst[(o * (rend - r) + k) * 8] in the nodes layout (indices r + position).  A walk stops
+    // at the subtree's end (its skip pointers reach rend only when it is done: stored as NN).  Exact in any
+    // order: the kernels keep the closest hit by (min t, max DFS triangle) and a box entered beyond it is
+    // skipped, and a shadow ray's verdict is any blocking hit.  The tree the orderings lay
+    // out: the reference's subtree as it is, or (walk_tree_sah, default) a binned-SAH tree over its leaves
+    // (build_sah: the same leaf boxes and node count)
+    auto near_first = [&](const uint32_t r, const uint32_t rend, std::vector<float>& dst) -> bool {
+        const uint32_t M = rend - r;
+        dst.assign((size_t)8 * M * 8, 0.0f);
+        std::vector<SNode> tn;
+        int troot = 0;
+        if (walk_tree_sah) {
+            std::vector<std::pair<Box, int>> leaves;
+            for (uint32_t i = r; i < rend; ++i)
+                if (fn[i].tri >= 0) leaves.emplace_back(fn[i].box, fn[i].tri);
+            tn.reserve(2 * leaves.size());
+            troot = build_sah(tn, leaves, 0, leaves.size());
+        } else {
+            tn.resize(M);
+            for (uint32_t i = r; i < rend; ++i) {
+                SNode& t = tn[i - r];
+                t.box = fn[i].box; t.tri = fn[i].tri; t.size = fn[i].skip - (int)i;
+                if (fn[i].tri < 0) { t.left = (int)(i + 1 - r); t.right = fn[i + 1].skip - (int)r; }
+            }
+        }
+        if (tn.size() != M) return err = "walk tree: node count differs from the subtree's", false;
+        auto centre = [](const Box& b, int a) { return a == 0 ? b.lo.x + b.hi.x : a == 1 ? b.lo.y + b.hi.y : b.lo.z + b.hi.z; };
+        std::vector<int> st;
+        for (uint32_t oct = 0; oct < 8; ++oct) {
+            float* base = &dst[(size_t)oct * M * 8];
+            uint32_t pos = 0;
+            st.assign(1, troot);
+            while (!st.empty()) {
+                const int i = st.back();
+                st.pop_back();
+                const SNode& n = tn[i];
+                uint32_t sk = r + pos + (uint32_t)n.size;   // the subtree of i occupies [pos, pos + size) of the ordering
+                if (sk >= rend) sk = NN;
+                float* q = base + 8 * (size_t)pos++;
+                q[0] = n.box.lo.x; q[1] = n.box.lo.y; q[2] = n.box.lo.z; q[3] = n.box.hi.x;
+                q[4] = n.box.hi.y; q[5] = n.box.hi.z; q[6] = bits_as_float((int32_t)sk); q[7] = bits_as_float(n.tri);
+                if (n.tri >= 0) continue;
+                const int a = n.left, b = n.right;
+                int ax = 0;
+                float best = -1.0f;
+                for (int k = 0; k < 3; ++k) {
+                    const float dk = std::fabs(centre(tn[a].box, k) - centre(tn[b].box, k));
+                    if (dk > best) { best = dk; ax = k; }
+                }
+                const bool neg = ((oct >> ax) & 1u) != 0u;
+                const bool a_first = (centre(tn[a].box, ax) <= centre(tn[b].box, ax)) != neg;
+                st.push_back(a_first ? b : a);
+                st.push_back(a_first ? a : b);
+            }
+        }
+        return true;
+    };
     // ---- split trace of a larger scene: the deepest internal node whose subtree leaves at most 32 leaves
     // outside it (the kernel keeps ray A's and ray B's outside candidates in the halves of one mask) (the subtrees with that property form the chain from the root down to it).  The outside
     // leaves are tested by their own boxes, exactly as the small scenes' leaf boxes above (every ancestor
@@ -600,62 +660,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             out.split_root = r;
             out.split_end = rend;
             out.stri = slots;
-            // near-first orderings of the walked subtree, one per direction octant (bit 0: d.x < 0, bit 1: d.y,
-            // bit 2: d.z): the same nodes in the pre-order that visits, at every internal node, first the child
-            // whose box centre lies nearer along the axis that separates the two centres most.  A walk stops
-            // at the subtree's end (its skip pointers reach split_end only when it is done: stored as NN).
-            // Exact in any order: the kernel keeps the closest hit by (min t, max DFS triangle) and a box
-            // entered beyond it is skipped, and a shadow ray's verdict is any blocking hit.
-            const uint32_t M = rend - r;
-            out.wcopies.assign((size_t)8 * M * 8, 0.0f);
-            // the tree the orderings lay out: the reference's subtree as it is, or (walk_tree_sah, default) a
-            // binned-SAH tree over its leaves (build_sah: the same leaf boxes and node count)
-            std::vector<SNode> tn;
-            int troot = 0;
-            if (walk_tree_sah) {
-                std::vector<std::pair<Box, int>> leaves;
-                for (uint32_t i = r; i < rend; ++i)
-                    if (fn[i].tri >= 0) leaves.emplace_back(fn[i].box, fn[i].tri);
-                tn.reserve(2 * leaves.size());
-                troot = build_sah(tn, leaves, 0, leaves.size());
-            } else {
-                tn.resize(M);
-                for (uint32_t i = r; i < rend; ++i) {
-                    SNode& t = tn[i - r];
-                    t.box = fn[i].box; t.tri = fn[i].tri; t.size = fn[i].skip - (int)i;
-                    if (fn[i].tri < 0) { t.left = (int)(i + 1 - r); t.right = fn[i + 1].skip - (int)r; }
-                }
-            }
-            if (tn.size() != M) return err = "walk tree: node count differs from the subtree's", false;
-            auto centre = [](const Box& b, int a) { return a == 0 ? b.lo.x + b.hi.x : a == 1 ? b.lo.y + b.hi.y : b.lo.z + b.hi.z; };
-            std::vector<int> st;
-            for (uint32_t oct = 0; oct < 8; ++oct) {
-                float* base = &out.wcopies[(size_t)oct * M * 8];
-                uint32_t pos = 0;
-                st.assign(1, troot);
-                while (!st.empty()) {
-                    const int i = st.back();
-                    st.pop_back();
-                    const SNode& n = tn[i];
-                    uint32_t sk = r + pos + (uint32_t)n.size;   // the subtree of i occupies [pos, pos + size) of the ordering
-                    if (sk >= rend) sk = NN;
-                    float* q = base + 8 * (size_t)pos++;
-                    q[0] = n.box.lo.x; q[1] = n.box.lo.y; q[2] = n.box.lo.z; q[3] = n.box.hi.x;
-                    q[4] = n.box.hi.y; q[5] = n.box.hi.z; q[6] = bits_as_float((int32_t)sk); q[7] = bits_as_float(n.tri);
-                    if (n.tri >= 0) continue;
-                    const int a = n.left, b = n.right;
-                    int ax = 0;
-                    float best = -1.0f;
-                    for (int k = 0; k < 3; ++k) {
-                        const float dk = std::fabs(centre(tn[a].box, k) - centre(tn[b].box, k));
-                        if (dk > best) { best = dk; ax = k; }
-                    }
-                    const bool neg = ((oct >> ax) & 1u) != 0u;
-                    const bool a_first = (centre(tn[a].box, ax) <= centre(tn[b].box, ax)) != neg;
-                    st.push_back(a_first ? b : a);
-                    st.push_back(a_first ? a : b);
-                }
-            }
+            if (!near_first(r, rend, out.wcopies)) return false;   // the walked subtree's near-first orderings
             out.sboxes.resize(uniq.size() * 8);
             for (size_t k = 0; k < uniq.size(); ++k) {
                 const Box& b = uniq[k].first;
@@ -665,6 +670,20 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
                 q[6] = bits_as_float((int32_t)(uint32_t)uniq[k].second); q[7] = bits_as_float((int32_t)(uint32_t)(uniq[k].second >> 32));
             }
         }
+    }
+    // ---- near-first orderings of the whole tree for the Whitted kernel (scenes with point lights, config C3):
+    // every internal box contains its children's (checked; with the tree's nesting every ancestor then
+    // contains a leaf box), so for a finite ray a leaf's own slab test decides whether the reference reaches
+    // it and any pre-order of any tree over the same leaf boxes visits the same candidates
+    out.worders.clear();
+    if (!lights_.empty() && NT > 64) {
+        bool nested = true;
+        auto inside = [](const Box& a, const Box& b) {   // b inside a
+            return a.lo.x <= b.lo.x && a.lo.y <= b.lo.y && a.lo.z <= b.lo.z && a.hi.x >= b.hi.x && a.hi.y >= b.hi.y && a.hi.z >= b.hi.z;
+        };
+        for (uint32_t i = 0; i < NN && nested; ++i)
+            if (fn[i].tri < 0) nested = inside(fn[i].box, fn[fn[i].left].box) && inside(fn[i].box, fn[fn[i].right].box);
+        if (nested && !near_first(0, NN, out.worders)) return false;
     }
     out.tris.resize((size_t)NT * 16);
     out.dbg_tri_f.resize((size_t)NT * 13);

@@ -58,6 +58,9 @@ struct FlatScene {
     // split scenes: the walked subtree in 8 near-first pre-orders (one per direction octant), the nodes
     // layout, node k of ordering o at [(o * (split_end - split_root) + k) * 8], indices as in `nodes`
     std::vector<float> wcopies;
+    // Whitted scenes (point lights): the whole tree in 8 near-first pre-orders, node k of ordering o at
+    // [(o * n_nodes + k) * 8] (empty: the kernel walks `nodes`)
+    std::vector<float> worders;
     std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
     std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag

@@ -32,6 +32,9 @@ namespace {
 #ifndef RT_WH_STEPS
 #define RT_WH_STEPS 8
 #endif
+#ifndef RT_WALK_PAIR
+#define RT_WALK_PAIR 0
+#endif
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
 
@@ -59,28 +62,49 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
             if (shadow) {
                 // (shadow_record.has_intersection) && (t * t < light_distance_squared), BV/Renderer.cpp:195
                 if (t * t < d2) { occluded = true; return true; }
-            } else if (t <= best) {
-                best = t; best_tri = tri;   // (left.t < right.t) ? left : right: the later leaf wins ties
+            } else if (t < best || (t == best && tri > best_tri)) {
+                // (left.t < right.t) ? left : right: the later DFS leaf wins ties -- triangles are numbered in
+                // DFS order, so in any walk order the winner is (min t, max triangle)
+                best = t; best_tri = tri;
             }
         }
         return false;
     };
     auto walk = [&](auto kind) {
         constexpr bool FIN = decltype(kind)::value;
+        // a finite ray walks the near-first ordering of its direction's octant when the scene has them
+        // (rt_scene.cpp near_first: the same leaf boxes, the closest hit found early, farther boxes skipped)
+        const float4* __restrict__ wn = nodes;
+        if (FIN && P.worders != nullptr) wn = P.worders + 2u * n * ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2));
         uint32_t i = 0;
         while (i < n) {
             const float bound = shadow ? sbound : ((best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff());
             int p0 = -1, p1 = -1;
-            for (uint32_t s = 0; s < RT_WH_STEPS && i < n; ++s) {
-                const float4 q0 = nodes[2 * i];
-                const float4 q1 = nodes[2 * i + 1];
+            auto test_node = [&](const float4 q0, const float4 q1) -> bool {   // false: two leaves postponed
                 if (COUNT) ++node_tests;
                 const bool hit = FIN ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound) : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                 const int tri = f2i(q1.w);
                 i = (hit && tri < 0) ? i + 1 : (uint32_t)f2i(q1.z);
                 if (hit && tri >= 0) {
                     if (p0 < 0) p0 = tri;
-                    else { p1 = tri; break; }
+                    else { p1 = tri; return false; }
+                }
+                return true;
+            };
+            if (RT_WALK_PAIR) {
+                // two nodes per dependent load (rt_coherent.hip RT_WALK_PAIR): node i and its pre-order successor
+                for (uint32_t s = 0; s < RT_WH_STEPS && i < n; ++s) {
+                    const uint32_t t0 = i, t1 = i + 1u < n ? i + 1u : i;
+                    const float4 q0 = wn[2 * t0], q1 = wn[2 * t0 + 1], q2 = wn[2 * t1], q3 = wn[2 * t1 + 1];
+                    if (!test_node(q0, q1)) break;
+                    if (i != t0 + 1u || i >= n) continue;
+                    if (!test_node(q2, q3)) break;
+                }
+            } else {
+                for (uint32_t s = 0; s < RT_WH_STEPS && i < n; ++s) {
+                    const float4 q0 = wn[2 * i];
+                    const float4 q1 = wn[2 * i + 1];
+                    if (!test_node(q0, q1)) break;
                 }
             }
             // the postponed leaves in DFS order (the later leaf still wins ties)

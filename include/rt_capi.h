@@ -127,6 +127,10 @@ rt_status rt_scene_lbvh_host(const rt_scene* s, float* nodes, float* tris);
  * layout (indices as in the DFS order; a skip pointer that leaves the subtree reads n_nodes).  *n_floats
  * receives the size (0: no split); out may be null to query it. */
 rt_status rt_scene_walk_orders(const rt_scene* s, float* out, uint64_t* n_floats);
+/* A Whitted scene's (point lights, config C3) whole tree in its 8 near-first pre-orders, for tests: 8 x n_nodes
+ * nodes in the same layout (a skip pointer past the last node reads n_nodes; 0 floats: none).  The Whitted
+ * kernel walks the ordering of a finite ray's octant (knob RT_WH_ORDER=0: the DFS order). */
+rt_status rt_scene_whitted_orders(const rt_scene* s, float* out, uint64_t* n_floats);
 
 /* ------------------------------------------------------------------ camera (host math) */
 typedef struct {

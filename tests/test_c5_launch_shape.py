@@ -11,7 +11,10 @@ oracle/_ref/ref_harness -- the reference's own MC/ BVH, triangle, material and c
 /root/reference, the Philox words injected into its mt19937 and re-filled at the top of a shading call
 for paths longer than one engine fill (oracle/ref/mt_inject.h) -- via `oracle/gen_golden.py full_c5`:
 the SHA-256 of the float4 accumulation and of the RGBA8 frame, and every 64th accumulation row.
-tests/golden/full_c5_4096.npz, when present, is the same at C5's full 4096 spp."""
+tests/golden/full_c5_4096.npz is the same at C5's full 4096 spp on every 64th row (`gen_golden.py full_c5_4096`:
+the harness renders only those rows -- the whole frame would take ~11 h on 8 cores); its SHA-256 covers those
+rows.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at the default budget) and
+compares the rows."""
 import hashlib
 import os
 
@@ -100,8 +103,11 @@ def test_c5_frame_in_launch_shape(scene, monkeypatch, name, budget_mb, min_passe
     same = np.all(bits(rows) == bits(z["accum_rows"]), axis=-1)
     assert same.all(), f"{same.mean():.6%} of the committed rows' pixels bitwise equal"
     assert np.array_equal(rgba[z["rows"]], z["rgba_rows"])
-    assert hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest() == str(z["sha_accum"])
-    assert hashlib.sha256(np.ascontiguousarray(rgba).tobytes()).hexdigest() == str(z["sha_rgba"])
+    rows_only = bool(z["rows_only"]) if "rows_only" in z.files else False
+    sel_acc = np.ascontiguousarray(acc[z["rows"]] if rows_only else acc)
+    sel_rgba = np.ascontiguousarray(rgba[z["rows"]] if rows_only else rgba)
+    assert hashlib.sha256(sel_acc.tobytes()).hexdigest() == str(z["sha_accum"])
+    assert hashlib.sha256(sel_rgba.tobytes()).hexdigest() == str(z["sha_rgba"])
 
 
 @pytest.mark.gpu

@@ -62,12 +62,13 @@ def slab(o, d):
     return hit
 
 
-def check_orders(sc, n_rays, seed, same_tree):
+def check_orders(sc, n_rays, seed, same_tree, whitted=False):
     info = sc.info()
-    r, e, NN = info.split_root, info.split_end, info.n_nodes
-    assert r > 0
+    NN = info.n_nodes
+    r, e = (0, NN) if whitted else (info.split_root, info.split_end)
+    assert whitted or r > 0
     boxes, skip, tri = original(sc)
-    Wall = sc.walk_orders()
+    Wall = sc.walk_orders(whitted=whitted)
     M = e - r
     assert Wall.shape == (8, M, 8)
     rows_of = lambda b, t, m: np.sort(np.concatenate([b[m], t[m, None].astype(np.float32)], axis=1).view(np.uint32), axis=0)
@@ -134,3 +135,15 @@ def test_walk_orders_of_c5(walk_tree, monkeypatch):
 
 def test_small_scenes_have_no_walk_orders():
     assert rt.Scene.cornell().walk_orders() is None
+    assert rt.Scene.cornell().walk_orders(whitted=True) is None
+
+
+@pytest.mark.parametrize("walk_tree", ["0", "1"], ids=["reference-tree", "sah-tree"])
+def test_whitted_orders_of_c3(walk_tree, monkeypatch):
+    """C3's whole tree (bunny + teapot, point lights) in the Whitted kernel's 8 near-first orderings
+    (rt_whitted.hip whitted_traverse; closest hit by (min t, max DFS triangle))."""
+    monkeypatch.setenv("RT_WALK_TREE", walk_tree)
+    z = np.load(SA.A.__file__.replace("test_skip_adversarial.py", "golden/bvh_scene.npz"))
+    sc = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"])
+    assert sc.walk_orders() is None   # no split: the path tracer's vertex kernel does not walk this scene
+    check_orders(sc, n_rays=30, seed=3, same_tree=walk_tree == "0", whitted=True)
