@@ -264,12 +264,6 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BVH_FOLD_DIV2
 #define RT_BVH_FOLD_DIV2 1
 #endif
-#ifndef RT_REC_FIRST
-#define RT_REC_FIRST 0
-#endif
-#ifndef RT_WALK_PAIR
-#define RT_WALK_PAIR 0
-#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -637,19 +631,15 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         // (a path ends at a vertex's service; a camera ray's service is its hit: !PRE, or the BVH variant's camera
         // rays the pre-pass left to it)
         const bool ends = served && ((PRE && !BVH) || pend) && (!cont || triA < 0 || emissive);
-        uint32_t rid = NO_REC;
-        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
-        // RT_REC_FIRST: the record loads are issued before the drain's ring loads, so both latencies overlap and
-        // the drain's parked-sample store comes after them (a load issued after a store waits for it);
-        // otherwise after the drain (the record's registers are then not live across the fold)
-        if constexpr (PRE && RT_REC_FIRST) {
-            rid = take_records(alive && (!in_path || ends));
-            if (rid != NO_REC) rec = kargs4().crec[rid];
-        }
         if (EXACT && __any(dleft != 0u || hasPend)) {
             if (dleft != 0u || hasPend) drain_step(dleft);
         }
-        if constexpr (PRE && !RT_REC_FIRST) {
+        // (after the drain's ring loads are folded: the record's registers are then not live across them.
+        // Issuing the record loads before the drain's, so that the two latencies overlap, measured -0.2 % at
+        // C4 256 spp, profiles/r05/ab/ab_c4_rec_first.json)
+        uint32_t rid = NO_REC;
+        float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (PRE) {
             rid = take_records(alive && (!in_path || ends));
             if (rid != NO_REC) rec = kargs4().crec[rid];
         }
@@ -1326,23 +1316,13 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             }
                             return true;
                         };
-                        if (RT_WALK_PAIR) {
-                            // two nodes per dependent load: node ti and its pre-order successor ti + 1, which the walk
-                            // visits next whenever ti is entered or is a leaf (a leaf's skip is ti + 1); the second
-                            // test is wasted when ti is a missed internal node
-                            for (uint32_t s = 0; s < steps && ti < tend; ++s) {
-                                const uint32_t t0 = ti, t1 = ti + 1u < tend ? ti + 1u : ti;
-                                const float4 q0 = wn[2 * t0], q1 = wn[2 * t0 + 1], q2 = wn[2 * t1], q3 = wn[2 * t1 + 1];
-                                if (!test_node(q0, q1)) break;
-                                if (ti != t0 + 1u || ti >= tend) continue;
-                                if (!test_node(q2, q3)) break;
-                            }
-                        } else {
-                            for (uint32_t s = 0; s < steps && ti < tend; ++s) {
-                                const float4 q0 = wn[2 * ti];
-                                const float4 q1 = wn[2 * ti + 1];
-                                if (!test_node(q0, q1)) break;
-                            }
+                        // (two nodes per dependent load -- node ti and its pre-order successor, visited next when ti is
+                        // entered or a leaf -- measured C5 -8 % at 7 waves (18 VGPRs spill) and -5 % at 6:
+                        // profiles/r05/ab/ab_c5_walk_pair.json)
+                        for (uint32_t s = 0; s < steps && ti < tend; ++s) {
+                            const float4 q0 = wn[2 * ti];
+                            const float4 q1 = wn[2 * ti + 1];
+                            if (!test_node(q0, q1)) break;
                         }
                     };
                     if (qround) walk_q();
