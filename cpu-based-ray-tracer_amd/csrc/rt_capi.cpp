@@ -118,7 +118,6 @@ struct rt_ctx {
     bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
     bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
     bool wh_order = true;     // Whitted kernel: walk the whole tree's near-first ordering of the ray's octant (RT_WH_ORDER=0: DFS)
-    uint32_t walk_mask = 7;   // A/B (RT_WALK_MASK): the ordering a ray walks is its octant & mask (fewer orderings in use)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
@@ -454,7 +453,6 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WH_ORDER")) c->wh_order = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = rt_knob("RT_WALK_MASK")) c->walk_mask = (uint32_t)std::strtoul(e, nullptr, 10) & 7u;
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
@@ -733,7 +731,6 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
             // offset so that node k of an ordering is at [2 * k] (k >= split_root; computed as an integer)
             P.wcopies = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(c->d_wcopies) - (uintptr_t)c->split_root * 2u * sizeof(float4));
             P.wcopy_stride = 2u * (c->split_end - c->split_root);
-            P.wcopy_mask = c->walk_mask;
         }
     }
     P.worders = c->d_worders;

@@ -264,6 +264,8 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BVH_FOLD_DIV2
 #define RT_BVH_FOLD_DIV2 1
 #endif
+// (the same for the direct term's two divisions in the BVH variant: C5 +0.1 %, within the spread --
+// profiles/r05/ab/ab_c5_nf_planes.json -- not kept)
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -1299,15 +1301,16 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             }
                         }
                     };
-                    auto walk = [&](auto kind) {
+                    auto walk = [&](auto kind, auto baked) {
                         // a split scene's ray with a finite reciprocal direction walks the subtree from its root:
-                        // in the near-first ordering of its direction's octant when the scene has them
-                        const float4* wn = S.nodes;
-                        if (Q.wcopies != nullptr && (decltype(kind)::value || finite3(r.rcp)))
-                            wn = Q.wcopies + (((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) & Q.wcopy_mask) * Q.wcopy_stride;
+                        // in the near-first ordering of its direction's octant when the scene has them, whose
+                        // boxes are stored as that octant's (near, far) planes (BAKED)
+                        constexpr bool BAKED = decltype(baked)::value;
+                        const float4* wn = BAKED ? Q.wcopies + ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) * Q.wcopy_stride : S.nodes;
                         auto test_node = [&](const float4 q0, const float4 q1) -> bool {   // true: go on to ti + 1
-                            const bool hit = decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
-                                                                   : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                            const bool hit = BAKED                    ? slab_nf_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
+                                             : decltype(kind)::value ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
+                                                                     : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                             const int tri = f2i(q1.w);
                             ti = (hit && tri < 0) ? ti + 1 : (uint32_t)f2i(q1.z);
                             if (hit && tri >= 0) {
@@ -1325,9 +1328,14 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             if (!test_node(q0, q1)) break;
                         }
                     };
+                    // (in a wave with a non-finite reciprocal the finite lanes still walk their ordering: a walk's
+                    // position spans rounds, and it indexes the ordering; the others walk the DFS array with the
+                    // general slab)
                     if (qround) walk_q();
-                    else if (fin) walk(FiniteSlab{});
-                    else walk(GeneralSlab{});
+                    else if (fin && Q.wcopies != nullptr) walk(FiniteSlab{}, std::true_type{});
+                    else if (fin) walk(FiniteSlab{}, std::false_type{});
+                    else if (Q.wcopies != nullptr && finite3(r.rcp)) walk(FiniteSlab{}, std::true_type{});
+                    else walk(GeneralSlab{}, std::false_type{});
                     SEC_MARK(6);   // BVH: the postponed leaves' tests in the MT section
 #if RT_SECTIONS
                     SEC_SUM(12, (uint32_t)(parked0 >= 0) + (uint32_t)(parked1 >= 0));   // BVH: leaves tested

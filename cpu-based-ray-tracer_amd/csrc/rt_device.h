@@ -268,6 +268,18 @@ __device__ __forceinline__ bool slab_hit_finite_within(const Ray& r, float lx, f
     const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
     return (tout >= 0.0f) && (tin <= tout) && (tin <= bound);
 }
+// slab_hit_finite_within on a box stored as its near and far planes for the ray's direction octant (the
+// near-first orderings, rt_scene.cpp near_first: x planes (hi, lo) when d.x < 0, else (lo, hi), ...): the
+// planes slab_hit_finite_within selects by the direction's signs, so the same subtractions, products,
+// max3/min3 and compares without the six selects
+__device__ __forceinline__ bool slab_nf_within(const Ray& r, float nx, float ny, float nz, float fx, float fy, float fz, float bound)
+{
+    const float tix = (nx - r.o.x) * r.rcp.x, tiy = (ny - r.o.y) * r.rcp.y, tiz = (nz - r.o.z) * r.rcp.z;
+    const float tox = (fx - r.o.x) * r.rcp.x, toy = (fy - r.o.y) * r.rcp.y, toz = (fz - r.o.z) * r.rcp.z;
+    const float tin = __builtin_fmaxf(tix, __builtin_fmaxf(tiy, tiz));
+    const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
+    return (tout >= 0.0f) && (tin <= tout) && (tin <= bound);
+}
 __device__ __forceinline__ bool rcp_finite(const Ray& r)
 {
     return __builtin_isfinite(r.rcp.x) && __builtin_isfinite(r.rcp.y) && __builtin_isfinite(r.rcp.z);

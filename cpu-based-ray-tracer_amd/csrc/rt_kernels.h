@@ -20,7 +20,8 @@ struct KParams {
     const float4* sboxes; const int32_t* stri; uint32_t n_sboxes, split_root, split_end, n_split_leaves;
     // the subtree's near-first orderings (rt_scene.h FlatScene::wcopies; null: off): ordering o's node k at
     // wcopies[2 * k + o * wcopy_stride], k in [split_root, split_end) (the pointer is offset by -2 * split_root)
-    const float4* wcopies; uint32_t wcopy_stride, wcopy_mask;   // ordering = octant & wcopy_mask (7; A/B: fewer in use)
+    // (each ordering's boxes are its octant's (near, far) planes: rt_device.h slab_nf_within)
+    const float4* wcopies; uint32_t wcopy_stride;
     // Whitted scenes: the whole tree's near-first orderings (FlatScene::worders; null: the DFS walk), ordering
     // o's node k at worders[2 * (o * n_nodes + k)]
     const float4* worders;

@@ -594,8 +594,12 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
                 uint32_t sk = r + pos + (uint32_t)n.size;   // the subtree of i occupies [pos, pos + size) of the ordering
                 if (sk >= rend) sk = NN;
                 float* q = base + 8 * (size_t)pos++;
-                q[0] = n.box.lo.x; q[1] = n.box.lo.y; q[2] = n.box.lo.z; q[3] = n.box.hi.x;
-                q[4] = n.box.hi.y; q[5] = n.box.hi.z; q[6] = bits_as_float((int32_t)sk); q[7] = bits_as_float(n.tri);
+                // the box as (near planes, far planes) for the octant's direction signs: x is (hi, lo) when
+                // d.x < 0 -- the planes the slab test selects for such a ray (rt_device.h slab_nf_within)
+                const bool sx = (oct & 1u) != 0u, sy = (oct & 2u) != 0u, sz = (oct & 4u) != 0u;
+                q[0] = sx ? n.box.hi.x : n.box.lo.x; q[1] = sy ? n.box.hi.y : n.box.lo.y; q[2] = sz ? n.box.hi.z : n.box.lo.z;
+                q[3] = sx ? n.box.lo.x : n.box.hi.x; q[4] = sy ? n.box.lo.y : n.box.hi.y; q[5] = sz ? n.box.lo.z : n.box.hi.z;
+                q[6] = bits_as_float((int32_t)sk); q[7] = bits_as_float(n.tri);
                 if (n.tri >= 0) continue;
                 const int a = n.left, b = n.right;
                 int ax = 0;

@@ -55,8 +55,10 @@ struct FlatScene {
     std::vector<float> sboxes;
     std::vector<int32_t> stri;
     uint32_t split_root = 0, split_end = 0;
-    // split scenes: the walked subtree in 8 near-first pre-orders (one per direction octant), the nodes
-    // layout, node k of ordering o at [(o * (split_end - split_root) + k) * 8], indices as in `nodes`
+    // split scenes: the walked subtree in 8 near-first pre-orders (one per direction octant), node k of
+    // ordering o at [(o * (split_end - split_root) + k) * 8], indices as in `nodes`; the nodes layout with
+    // each box as (near.xyz, far.x)(far.y, far.z, skip, tri), near/far the planes a ray of octant o meets
+    // first/last (x: (hi, lo) when bit 0 -- d.x < 0 -- is set)
     std::vector<float> wcopies;
     // Whitted scenes (point lights): the whole tree in 8 near-first pre-orders, node k of ordering o at
     // [(o * n_nodes + k) * 8] (empty: the kernel walks `nodes`)

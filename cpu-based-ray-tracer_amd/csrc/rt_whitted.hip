@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rt_device.h"
 #include "rt_kernels.h"
 #include "rt_layout.h"
@@ -32,14 +34,7 @@ namespace {
 #ifndef RT_WH_STEPS
 #define RT_WH_STEPS 8
 #endif
-// two point lights' shadow rays walked together (whitted_shadow2)
-#ifndef RT_WH_SHADOW2
-#define RT_WH_SHADOW2 0
-#endif
-// minimum waves per SIMD of whitted_kernel's register allocation
-#ifndef RT_WH_MIN_WAVES
-#define RT_WH_MIN_WAVES 8
-#endif
+
 
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
@@ -76,19 +71,21 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
         }
         return false;
     };
-    auto walk = [&](auto kind) {
+    auto walk = [&](auto kind, auto baked) {
         constexpr bool FIN = decltype(kind)::value;
         // a finite ray walks the near-first ordering of its direction's octant when the scene has them
-        // (rt_scene.cpp near_first: the same leaf boxes, the closest hit found early, farther boxes skipped)
-        const float4* __restrict__ wn = nodes;
-        if (FIN && P.worders != nullptr) wn = P.worders + 2u * n * ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2));
+        // (rt_scene.cpp near_first: the same leaf boxes, the closest hit found early, farther boxes skipped),
+        // whose boxes are stored as the octant's (near, far) planes (BAKED, rt_device.h slab_nf_within)
+        constexpr bool BAKED = decltype(baked)::value;
+        const float4* __restrict__ wn = BAKED ? P.worders + 2u * n * ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2)) : nodes;
         uint32_t i = 0;
         while (i < n) {
             const float bound = shadow ? sbound : ((best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff());
             int p0 = -1, p1 = -1;
             auto test_node = [&](const float4 q0, const float4 q1) -> bool {   // false: two leaves postponed
                 if (COUNT) ++node_tests;
-                const bool hit = FIN ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound) : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
+                const bool hit = BAKED ? slab_nf_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound)
+                                 : FIN ? slab_hit_finite_within(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, bound) : slab_hit(r, q0.x, q0.y, q0.z, q0.w, q1.x, q1.y);
                 const int tri = f2i(q1.w);
                 i = (hit && tri < 0) ? i + 1 : (uint32_t)f2i(q1.z);
                 if (hit && tri >= 0) {
@@ -108,70 +105,9 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
             if (p1 >= 0 && tri_test(p1)) return;
         }
     };
-    if (rcp_finite(r)) walk(FiniteSlab{});
-    else walk(GeneralSlab{});
-}
-
-// two shadow rays from one shading point (two point lights) walked together: each step issues both rays'
-// node loads before either is tested, so a lane has two dependent-load chains in flight instead of one (the
-// walk is latency-bound: profiles/r05/c3).  Per ray exactly whitted_traverse's shadow walk -- its own
-// ordering, bound and any-hit verdict (t * t < d2, BV/Renderer.cpp:195) -- so each verdict is unchanged.
-// Both reciprocal directions must be finite (the caller falls back to whitted_traverse otherwise).
-template <bool COUNT>
-__device__ __forceinline__ void whitted_shadow2(const KParams& P, const V3& o, const Ray& ra, const Ray& rb, double d2a, double d2b, bool& occA,
-                                                bool& occB, uint32_t& node_tests, uint32_t& tri_tests)
-{
-    const float4* __restrict__ tris = P.tris;
-    const uint32_t n = P.n_nodes;
-    // one base for both rays, each ray's ordering as a 32-bit node offset (fewer registers than two pointers)
-    const float4* __restrict__ wn = P.worders == nullptr ? P.nodes : P.worders;
-    auto order = [&](const Ray& r) -> uint32_t {
-        return P.worders == nullptr ? 0u : 2u * n * ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2));
-    };
-    const uint32_t oa = order(ra), ob = order(rb);
-    uint32_t ia = 0, ib = 0;
-    occA = false; occB = false;
-    while (ia < n || ib < n) {
-        // (the bounds and the reciprocal directions recomputed per round rather than kept live across the
-        // postponed leaves' tests)
-        const float ba = __builtin_sqrtf((float)d2a) * 1.00001f + 1e-5f, bb = __builtin_sqrtf((float)d2b) * 1.00001f + 1e-5f;
-        const Ray qa = make_ray(o, ra.d), qb = make_ray(o, rb.d);
-        int pa0 = -1, pa1 = -1, pb0 = -1, pb1 = -1;
-        for (uint32_t s = 0; s < RT_WH_STEPS; ++s) {
-            const bool ga = ia < n && pa1 < 0, gb = ib < n && pb1 < 0;
-            if (!ga && !gb) break;
-            const uint32_t ja = oa + 2u * (ga ? ia : 0u), jb = ob + 2u * (gb ? ib : 0u);
-            const float4 qa0 = wn[ja], qa1 = wn[ja + 1], qb0 = wn[jb], qb1 = wn[jb + 1];
-            if (ga) {
-                if (COUNT) ++node_tests;
-                const bool hit = slab_hit_finite_within(qa, qa0.x, qa0.y, qa0.z, qa0.w, qa1.x, qa1.y, ba);
-                const int tri = f2i(qa1.w);
-                ia = (hit && tri < 0) ? ia + 1 : (uint32_t)f2i(qa1.z);
-                if (hit && tri >= 0) { if (pa0 < 0) pa0 = tri; else pa1 = tri; }
-            }
-            if (gb) {
-                if (COUNT) ++node_tests;
-                const bool hit = slab_hit_finite_within(qb, qb0.x, qb0.y, qb0.z, qb0.w, qb1.x, qb1.y, bb);
-                const int tri = f2i(qb1.w);
-                ib = (hit && tri < 0) ? ib + 1 : (uint32_t)f2i(qb1.z);
-                if (hit && tri >= 0) { if (pb0 < 0) pb0 = tri; else pb1 = tri; }
-            }
-        }
-        // the postponed leaves: slots 0-1 ray a's, 2-3 ray b's (one Moller-Trumbore body in the loop)
-#pragma nounroll
-        for (int k = 0; k < 4; ++k) {
-            const int tri = k == 0 ? pa0 : k == 1 ? pa1 : k == 2 ? pb0 : pb1;
-            const bool isA = k < 2;
-            if (tri < 0 || (isA ? occA : occB)) continue;
-            if (COUNT) ++tri_tests;
-            const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
-            double t;
-            if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, isA ? ra.d : rb.d, t) && t * t < (isA ? d2a : d2b)) {
-                if (isA) { occA = true; ia = n; }
-                else { occB = true; ib = n; }
-            }
-        }
-    }
+    if (!rcp_finite(r)) walk(GeneralSlab{}, std::false_type{});
+    else if (P.worders != nullptr) walk(FiniteSlab{}, std::true_type{});
+    else walk(FiniteSlab{}, std::false_type{});
 }
 
 }  // namespace
@@ -218,43 +154,10 @@ __device__ __forceinline__ V3 whitted_sample(const KParams& P, uint32_t lx, uint
         const V3 off = muls(n, INTERSECTION_CORRECTION);
         const V3 sp = (dot(ray.d, n) < 0.0f) ? add(x, off) : sub(x, off);
         V3 diffuse{0.0f, 0.0f, 0.0f};
-        uint32_t l = 0;
-        if (RT_WH_SHADOW2) {
-            // lights in pairs: both shadow rays walked together, the diffuse terms added in light order
-            for (; l + 2u <= P.n_plights; l += 2u) {
-                const float4 lp0 = P.plights[2 * l], lp1 = P.plights[2 * l + 2];
-                V3 l0 = sub(V3{lp0.x, lp0.y, lp0.z}, x), l1 = sub(V3{lp1.x, lp1.y, lp1.z}, x);
-                const float d20 = dot(l0, l0), d21 = dot(l1, l1);
-                l0 = w_normalize(l0);
-                l1 = w_normalize(l1);
-                const Ray s0 = make_ray(sp, l0), s1 = make_ray(sp, l1);
-                if (COUNT) rays += 2;
-                bool b0 = false, b1 = false;
-                if (rcp_finite(s0) && rcp_finite(s1)) {
-                    whitted_shadow2<COUNT>(P, sp, s0, s1, (double)d20, (double)d21, b0, b1, node_tests, tri_tests);
-                } else {
-                    double sb = 1.7976931348623157e308;
-                    int st = -1;
-                    whitted_traverse<COUNT>(P, s0, true, (double)d20, sb, st, b0, node_tests, tri_tests);
-                    sb = 1.7976931348623157e308;
-                    whitted_traverse<COUNT>(P, s1, true, (double)d21, sb, st, b1, node_tests, tri_tests);
-                }
-                // (the radiances and the normal read after the walks: not live across them)
-                const float4 tn2 = P.tris[4 * best_tri + 3];
-                const V3 n2{tn2.x, tn2.y, tn2.z};
-                if (!b0) {
-                    const float4 lr0 = P.plights[2 * l + 1];
-                    const float c = __builtin_fabsf(dot(l0, n2));
-                    diffuse = add(diffuse, V3{lr0.x * c, lr0.y * c, lr0.z * c});
-                }
-                if (!b1) {
-                    const float4 lr1 = P.plights[2 * l + 3];
-                    const float c = __builtin_fabsf(dot(l1, n2));
-                    diffuse = add(diffuse, V3{lr1.x * c, lr1.y * c, lr1.z * c});
-                }
-            }
-        }
-        for (; l < P.n_plights; ++l) {
+        // (the two lights' shadow rays walked together -- both rays' node loads issued before either test --
+        // measured 2-7 % slower at 6-8 waves per SIMD: 4-32 VGPRs spill; 7 waves alone -1.4 %,
+        // profiles/r05/ab/ab_c3_shadow2_waves.json)
+        for (uint32_t l = 0; l < P.n_plights; ++l) {
             const float4 lp = P.plights[2 * l], lr4 = P.plights[2 * l + 1];
             V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
             const float d2 = dot(ld, ld);
@@ -285,7 +188,7 @@ __device__ __forceinline__ void whitted_store(const KParams& P, uint32_t local, 
 }
 
 template <bool COUNT>
-__global__ void __launch_bounds__(256, RT_WH_MIN_WAVES) whitted_kernel(KParams P)
+__global__ void __launch_bounds__(256, 8) whitted_kernel(KParams P)
 {
     uint32_t node_tests = 0, tri_tests = 0, rays = 0;
     constexpr uint32_t FG = WH_FG;

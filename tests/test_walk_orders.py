@@ -30,9 +30,14 @@ def original(sc):
     return nf[:, :6].copy(), np.arange(n) + size, ni[:, 2].copy()
 
 
-def copy_fields(W):
-    """one ordering's (boxes, skip, tri) from its traversal-layout rows"""
-    return W[:, :6].copy(), W[:, 6].view(np.int32).astype(np.int64), W[:, 7].view(np.int32).astype(np.int64)
+def copy_fields(W, octant):
+    """one ordering's (boxes as lo.xyz hi.xyz, skip, tri) from its rows, whose boxes are stored as the octant's
+    (near.xyz, far.xyz) planes: axis a's planes are (hi, lo) when bit a of the octant (d_a < 0) is set"""
+    near, far = W[:, 0:3], W[:, 3:6]
+    neg = np.array([(octant >> a) & 1 for a in range(3)], bool)
+    lo = np.where(neg, far, near)
+    hi = np.where(neg, near, far)
+    return np.concatenate([lo, hi], axis=1), W[:, 6].view(np.int32).astype(np.int64), W[:, 7].view(np.int32).astype(np.int64)
 
 
 def walk(boxes, skip, tri, start, stop, base, hit):
@@ -77,7 +82,7 @@ def check_orders(sc, n_rays, seed, same_tree, whitted=False):
     rng = np.random.default_rng(seed)
     lo, hi = boxes[r, :3].astype(np.float64), boxes[r, 3:].astype(np.float64)
     for oct_ in range(8):
-        bx, sk, tr = copy_fields(Wall[oct_])
+        bx, sk, tr = copy_fields(Wall[oct_], oct_)
         # the same leaves (box, triangle), each once; for the reference's tree every node
         assert len(bx) == M
         rows = rows_of(bx, tr, np.ones(M, bool) if same_tree else tr >= 0)
@@ -111,7 +116,7 @@ def check_orders(sc, n_rays, seed, same_tree, whitted=False):
         oct_ = int(d[0] < 0) | int(d[1] < 0) << 1 | int(d[2] < 0) << 2
         hit = slab(o, d)
         ref_leaves, ref_visits = walk(boxes, skip, tri, r, e, 0, hit)
-        bx, sk, tr = copy_fields(Wall[oct_])
+        bx, sk, tr = copy_fields(Wall[oct_], oct_)
         leaves, visits = walk(bx, sk, tr, r, NN, r, hit)
         assert sorted(leaves) == sorted(ref_leaves)
         if same_tree:
