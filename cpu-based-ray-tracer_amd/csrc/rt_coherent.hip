@@ -247,6 +247,7 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_DRAIN_BATCH
 #define RT_DRAIN_BATCH 2
 #endif
+
 // pending fold (leaf-box variant, EXACT): a path that ends while the lane's previous fold still drains parks
 // its own fold behind it (one ring slot holds its L and frame index) instead of completing the draining one
 // at once -- that completion ran a whole fold loop for the one or two lanes that needed it in 83 % of the
@@ -633,6 +634,8 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         // (a path ends at a vertex's service; a camera ray's service is its hit: !PRE, or the BVH variant's camera
         // rays the pre-pass left to it)
         const bool ends = served && ((PRE && !BVH) || pend) && (!cont || triA < 0 || emissive);
+        // (as many fold levels as the wave's deepest drain needs instead of DRAIN_STEP, a wave-uniform choice
+        // of 1 / 2 / 3: C4 -0.4 %, C5 +-0, profiles/r05/ab/ab_c{4,5}_drain_adapt.json)
         if (EXACT && __any(dleft != 0u || hasPend)) {
             if (dleft != 0u || hasPend) drain_step(dleft);
         }
