@@ -3,8 +3,10 @@ two and eight ranks on the box's one GPU: each rank renders its row bands with t
 all-gathered (gloo on host-staged bands: RCCL needs one GPU per rank) and reassembled on rank 0; the
 time is the MAX over ranks.  The JSON line must report the whole job (n_gpus 2, both ranks' times, value
 from the slowest) and rank 0's reassembled frame must equal the one-rank frame bit for bit (the RNG is
-keyed by the global pixel).  The RCCL branch itself (one GPU per rank) runs only on a
-multi-GPU node (the driver's scaling run)."""
+keyed by the global pixel).  The RCCL branch's calls (init_process_group("nccl"), the
+all_gather_into_tensor and the MAX all-reduce) run here with one rank (`--force-dist`,
+test_bench_rccl_branch_one_rank); their multi-rank data movement runs only on a multi-GPU node (the
+driver's scaling run)."""
 import json
 import os
 import socket
