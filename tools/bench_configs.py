@@ -65,6 +65,28 @@ def counters_for(kname, W, H, spp, mode, passes):
     return None
 
 
+def c5_parity(ctx, W, H, spp):
+    """C5's timed frame against the reference harness's: the rows of
+    tests/golden/full_c5.npz (256 spp, whole frame hashed) or full_c5_4096.npz (4096 spp, every 64th row
+    hashed) bitwise, as bench.py's parity field does for C4; None when no fixture has this shape."""
+    import hashlib
+    for name in ("full_c5", "full_c5_4096"):
+        p = os.path.join(REPO, "tests", "golden", f"{name}.npz")
+        if not os.path.exists(p):
+            continue
+        z = np.load(p)
+        if (int(z["W"]), int(z["H"]), int(z["spp"])) != (W, H, spp):
+            continue
+        acc = ctx.accumulation()
+        rows = z["rows"]
+        same = np.all(acc[rows, :, :3].view(np.uint32) == z["accum_rows"].view(np.uint32), axis=-1)
+        sel = np.ascontiguousarray(acc[rows] if bool(z["rows_only"]) else acc)
+        return {"fixture": f"tests/golden/{name}.npz", "rows_checked": int(len(rows)), "bitwise_frac": round(float(same.mean()), 6),
+                "sha_accum_match": hashlib.sha256(sel.tobytes()).hexdigest() == str(z["sha_accum"]),
+                "scope": "every 64th row" if bool(z["rows_only"]) else "whole frame"}
+    return None
+
+
 def flops_per_sample(c):
     if c in WHITTED_FLOPS:
         return WHITTED_FLOPS[c]
@@ -155,10 +177,13 @@ def main():
         mode = "whitted" if c in ("C1", "C3") else ("fast" if args.fast else "exact")
         if roof is not None:
             roof["counters"] = counters_for(rt.KERNEL_NAMES.get(st.kernel, str(st.kernel)), W, H, spp, mode, st.n_passes)
-        print(json.dumps({"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
-                          "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "passes": st.n_passes,
-                          "prepass_ms": round(st.last_prepass_ms, 3), "path_ms": round(st.last_main_ms, 3), "roofline": roof,
-                          "mode": mode}), flush=True)
+        line = {"config": c, "width": W, "height": H, "spp": spp, "kernel_ms": round(ms, 3),
+                "msamples_per_s": round(rate / 1e6, 2), "grid": st.grid, "passes": st.n_passes,
+                "prepass_ms": round(st.last_prepass_ms, 3), "path_ms": round(st.last_main_ms, 3), "roofline": roof,
+                "mode": mode}
+        if c == "C5" and not args.fast:
+            line["parity"] = c5_parity(ctx, W, H, spp)   # the last timed render's accumulation (seed 0, RR 0.8, frames 1..spp)
+        print(json.dumps(line), flush=True)
         ctx.close()
 
 
