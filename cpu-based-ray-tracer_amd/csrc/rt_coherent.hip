@@ -896,10 +896,10 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     int lt = 0;
                     sample_light(S, Q.light_area, G, q, nl0, nullptr, &lt);
                     const V3 p2q = sub(q, p);
-                    const V3 wl = glm_normalize(p2q);
+                    const V3 wl = glm_normalize_wave(p2q);
                     const V3 nl = (dot(nl0, neg(wl)) < 0.0f) ? neg(nl0) : nl0;
                     const float sc1 = dot(wl, n), sc2 = dot(neg(wl), nl), sd2 = dot(p2q, p2q);
-                    slen = glm_length(p2q);
+                    slen = sqrt_wave(dot(p2q, p2q));   // glm_length (the square root the normalize took)
                     // the unoccluded direct term; the shadow verdict selects it (BRDF: MC/WhittedMaterial.h:58-69)
                     const float4 mb = S.mats[2 * mat];
                     const V3 f = (sc1 >= 0.0f) ? V3{mb.x, mb.y, mb.z} : V3{0.0f, 0.0f, 0.0f};
@@ -928,7 +928,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 // Russian roulette + indirect direction (the depth cap only bounds the loop: P = rr^4096)
                 cont = G.next() < Q.rr && depth < 4096u;
                 if (cont) {
-                    const V3 wi = glm_normalize(sample_hemisphere(n, G));
+                    const V3 wi = glm_normalize_big(sample_hemisphere(n, G));   // (a unit vector up to rounding, or NaN)
                     lsf(VS_PCOS) = dot(wi, n);
                     dA = wi;
                 }
@@ -965,11 +965,11 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             cy = cy * 2.0f - 1.0f;
             float tg[4];
             mat4_mul(Q.iproj, cx, cy, 1.0f, 1.0f, tg);
-            const V3 dv = glm_normalize(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], IEEE_DIV ? 0.0f : rcp_f32(tg[3])));
+            const V3 dv = glm_normalize_wave(vdiv(V3{tg[0], tg[1], tg[2]}, tg[3], IEEE_DIV ? 0.0f : rcp_f32(tg[3])));
             float wd[4];
             mat4_mul(Q.iview, dv.x, dv.y, dv.z, 0.0f, wd);
             o = V3{Q.cam_pos[0], Q.cam_pos[1], Q.cam_pos[2]};
-            dA = w_normalize(V3{wd[0], wd[1], wd[2]});
+            dA = w_normalize_wave(V3{wd[0], wd[1], wd[2]});
             hasA = true; hasB = false;
             depth = 0;
             pend = false;
@@ -1598,10 +1598,10 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
             dq = div1_core(txyz, tg[3], rcp_f32_mid(tg[3]));
         else
             dq = divs_fast(txyz, tg[3], rcp_f32(tg[3]));
-        const V3 dv = glm_normalize(dq);
+        const V3 dv = glm_normalize_wave(dq);
         float wd[4];
         mat4_mul(P.iview, dv.x, dv.y, dv.z, 0.0f, wd);
-        const V3 d = w_normalize(V3{wd[0], wd[1], wd[2]});
+        const V3 d = w_normalize_wave(V3{wd[0], wd[1], wd[2]});
         const Ray r = make_ray(o, d);
         // closest hit, the later leaf winning ties (MC/BVH.h:97-100)
         double t = 1.7976931348623157e308;

@@ -125,14 +125,46 @@ __device__ __forceinline__ float div1_core(float x, float d, float y)
 __device__ __forceinline__ V3 div1_core(V3 a, float d, float y) { return V3{div1_core(a.x, d, y), div1_core(a.y, d, y), div1_core(a.z, d, y)}; }
 constexpr uint32_t kBits2m100 = 0x0D800000u, kBits2p100 = 0x71800000u;   // bits(2^-100), bits(2^100)
 
+// sqrt for x = +-0 or x >= 2^-96 (and +inf, NaN): the compiler's correctly rounded sequence under
+// -fhip-fp32-correctly-rounded-divide-sqrt -- v_sqrt_f32, then one ulp down or up by the sign of the fma
+// residual -- without its input scaling, which only inputs below 2^-96 take, and its final class test,
+// which returns x for +-0 and +inf, values the sequence already gives.  Every such float gives the bits of
+// __builtin_sqrtf (tools/verify_sqrt.hip checks them all); 8 instructions fewer per square root.
+#ifndef RT_FAST_SQRT
+#define RT_FAST_SQRT 1   // 0: __builtin_sqrtf everywhere (A/B)
+#endif
+__device__ __forceinline__ float sqrt_big(float x)
+{
+    if (!RT_FAST_SQRT) return __builtin_sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __int_as_float(__float_as_int(s) - 1);
+    const float s1 = (__builtin_fmaf(-sdn, s, x) <= 0.0f) ? sdn : s;
+    const float sup = __int_as_float(__float_as_int(s) + 1);
+    return (__builtin_fmaf(-sup, s, x) > 0.0f) ? sup : s1;
+}
+// the argument range of sqrt_big
+__device__ __forceinline__ bool sqrt_big_ok(float x) { return x >= 0x1p-96f || x == 0.0f; }
+// sqrt(x) by sqrt_big when every active lane's x lies in its range (one wave-uniform test), else __builtin_sqrtf
+__device__ __forceinline__ float sqrt_wave(float x) { return (RT_FAST_SQRT && __all(sqrt_big_ok(x))) ? sqrt_big(x) : __builtin_sqrtf(x); }
+
 // glm::normalize = v * (1 / sqrt(dot(v,v))), GLM/detail/func_geometric.inl:82-90, func_exponential.inl:136-139
 __device__ __forceinline__ V3 glm_normalize(V3 v) { float is = rcp_f32(__builtin_sqrtf(dot(v, v))); return muls(v, is); }
 __device__ __forceinline__ float glm_length(V3 v) { return __builtin_sqrtf(dot(v, v)); }
+// the same with sqrt_big, for vectors whose squared length is provably 0, NaN, +inf or >= 2^-96 (unit
+// directions, unit normals' components), and with sqrt_wave for any vector
+__device__ __forceinline__ V3 glm_normalize_big(V3 v) { float is = rcp_f32(sqrt_big(dot(v, v))); return muls(v, is); }
+__device__ __forceinline__ V3 glm_normalize_wave(V3 v) { float is = rcp_f32(sqrt_wave(dot(v, v))); return muls(v, is); }
 // Whitted::normalize (zero-safe), MC/VectorFloat.h:22-31
 __device__ __forceinline__ V3 w_normalize(V3 v)
 {
     float l2 = ((v.x * v.x) + (v.y * v.y)) + (v.z * v.z);
     if (l2 > 0.0f) { float inv = rcp_f32(__builtin_sqrtf(l2)); return V3{v.x * inv, v.y * inv, v.z * inv}; }
+    return v;
+}
+__device__ __forceinline__ V3 w_normalize_wave(V3 v)
+{
+    float l2 = ((v.x * v.x) + (v.y * v.y)) + (v.z * v.z);
+    if (l2 > 0.0f) { float inv = rcp_f32(sqrt_wave(l2)); return V3{v.x * inv, v.y * inv, v.z * inv}; }
     return v;
 }
 // std::max / std::min / glm::max / glm::min: compare-select, the first operand survives a NaN

@@ -132,7 +132,7 @@ __device__ __forceinline__ void sample_light(const SceneView& S, float light_are
     }
     const int lt = f2i(S.lnodes[node].w);
     const float4 A = S.ltris[4 * lt], B = S.ltris[4 * lt + 1], C = S.ltris[4 * lt + 2], N = S.ltris[4 * lt + 3];
-    const float x = 1.0f - __builtin_sqrtf(g.next());
+    const float x = 1.0f - sqrt_big(g.next());   // (a draw is 0 or in [2^-32, 1]: sqrt_big's range)
     const float y = g.next();
     const V3 a{A.x, A.y, A.z}, b{B.x, B.y, B.z}, c{C.x, C.y, C.z};
     q = add(add(smul(x, a), smul((1.0f - x) * y, b)), smul((1.0f - x) * (1.0f - y), c));
@@ -146,15 +146,17 @@ template <class G>
 __device__ __forceinline__ V3 sample_hemisphere(V3 n, G& g)
 {
     const float z = g.next();
-    const float rxy = __builtin_sqrtf(1.0f - z * z);
+    const float rxy = sqrt_big(1.0f - z * z);   // (z a draw in [0, 1]: 1 - z * z is 0 or >= 2^-23)
     const float phi = 2.0f * PI_F * g.next();
     float cphi, sphi;
     sincos_f(phi, cphi, sphi);
     const float x = rxy * cphi;
     const float y = rxy * sphi;
     V3 Y;
-    if (__builtin_fabsf(n.x) > __builtin_fabsf(n.y)) Y = glm_normalize(V3{n.z, 0.0f, -(n.x)});
-    else Y = glm_normalize(V3{0.0f, n.z, -(n.y)});
+    // (n a unit normal, NaN or infinite for a degenerate triangle: the squared length is >= 1/2 up to
+    // rounding, NaN or +inf, inside sqrt_big's range)
+    if (__builtin_fabsf(n.x) > __builtin_fabsf(n.y)) Y = glm_normalize_big(V3{n.z, 0.0f, -(n.x)});
+    else Y = glm_normalize_big(V3{0.0f, n.z, -(n.y)});
     const V3 X = cross(Y, n);
     return add(add(smul(x, X), smul(y, Y)), smul(z, n));
 }
