@@ -123,10 +123,13 @@ struct rt_ctx {
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
     uint32_t vthresh = 32, vsteps = 8; // the same for the vertex kernel's BVH variant (C5 sweep)
-    uint32_t sthresh = 8, ssteps = 12; // the BVH variant with the split trace: few lanes walk, so rounds run while
-                                       // more than 8 of them do (C5 sweep 2 / 4 / 6 / 8 / 12 / 16 / 32: 3003 / 3283 /
-                                       // 3399 / 3419-3427 / 3403 / 3261 / 2588 Msamples/s), 12 box tests per round
-                                       // (4 / 8 / 12 / 16: 3336 / 3427 / 3466 / 3461; profiles/r03/ab/ab_c5_split.json)
+    uint32_t sthresh = 12, ssteps = 12; // the BVH variant with the split trace: few lanes walk, so rounds run while
+                                       // more than 12 of them do, 12 box tests per round.  Round 3 (C5 sweep 2 / 4 / 6 /
+                                       // 8 / 12 / 16 / 32: 3003 / 3283 / 3399 / 3419-3427 / 3403 / 3261 / 2588 Msamples/s;
+                                       // steps 4 / 8 / 12 / 16: 3336 / 3427 / 3466 / 3461, profiles/r03/ab/ab_c5_split.json)
+                                       // chose 8; on the round-5 kernel (near-first SAH walk, shorter walks) 8 / 12 / 16 /
+                                       // 20 / 24 / 32 give 87.7-88.4 / 85.8 / 86.4 / 88.5 / 92.0 / 102.5 ms at 3840x2160x64
+                                       // (profiles/r05/ab/sweep_c5_thresh.jsonl)
 };
 
 namespace {

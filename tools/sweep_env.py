@@ -23,7 +23,7 @@ KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERT
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--set", action="append", default=[], help="space/comma separated K=V assignments for one variant")
+    ap.add_argument("--set", action="append", default=[], help="space/comma/colon separated K=V assignments for one variant")
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -44,7 +44,7 @@ def main():
     for v in variants:
         for k in KNOBS:
             os.environ.pop(k, None)
-        for a in v.replace(",", " ").split():
+        for a in v.replace(",", " ").replace(":", " ").split():   # (":" too: tools/gpu_run.sh splits its steps on commas)
             k, val = a.split("=")
             os.environ[k] = val
         # the scene is built under the variant's knobs too (RT_WALK_TREE is read by the scene build)
