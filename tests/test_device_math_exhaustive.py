@@ -1,0 +1,30 @@
+"""Exhaustive checks of the kernels' short arithmetic sequences on the device, over every float they can take
+(tools/verify_rcp.hip, tools/verify_sqrt.hip, built by __graft_entry__.build()):
+  * rcp_f64_of_f32 (Moller-Trumbore's 1 / (double)den: v_rcp_f64 + two Newton steps) and rcp_f32 (v_rcp_f32
+    + one Newton step inside [2^-126, 2^126)) against the IEEE divisions, all 2^32 float patterns;
+  * sqrt_big (v_sqrt_f32 + the one-ulp correction, without the compiler's input scaling and class test)
+    against __builtin_sqrtf under -fhip-fp32-correctly-rounded-divide-sqrt, every pattern of its range.
+Bit for bit; each binary exits non-zero on a mismatch."""
+import json
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["verify_rcp", "verify_sqrt"])
+def test_short_sequences_match_ieee_on_every_float(name):
+    exe = os.path.join(REPO, "tools", name)
+    assert os.path.exists(exe), f"{exe} missing: run __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=180)
+    line = r.stdout.strip().splitlines()[-1]
+    print(line)
+    d = json.loads(line)
+    assert r.returncode == 0, line
+    if name == "verify_rcp":
+        assert d["rcp_f64_of_f32"] == 0 and d["rcp_f32"] == 0
+    else:
+        assert d["mismatches"] == 0 and d["patterns_checked"] > 1_800_000_000
