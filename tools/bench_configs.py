@@ -113,7 +113,10 @@ def main():
     ap.add_argument("--c5-spp", type=int, default=64)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--full-warmup", action="store_true", help="warm up at the measured spp (steady-state buffers)")
+    ap.add_argument("--lib", default=None, help="library file in the package directory (A/B builds; default librt_hip.so)")
     args = ap.parse_args()
+    if args.lib:
+        rt.LIB_PATH = os.path.join(REPO, "cpu-based-ray-tracer_amd", args.lib)
     bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
     for c in args.configs.split(","):
         if c.startswith("DN"):
