@@ -74,7 +74,7 @@ __device__ __forceinline__ void jbf_tap(const JbfConsts& K, const V3& cc, const 
     const float xp = dot(dp, dp);
     const V3 dc = sub(kcol, cc);
     const float xc = dot(dc, dc);
-    float cop = dot(cn, glm_normalize_wave(dp));   // (the short square root when every lane's |dp|^2 allows it)
+    float cop = dot(cn, glm_normalize(dp));   // (the short square root here measured neutral: profiles/r05/ab/dn_sqrt_ab.jsonl)
     cop = cop * cop;
     float wpd, cd, cq;
     if (K.fast && __all(div_range(xp) && div_range(xc) && div_range(cop))) {
