@@ -203,10 +203,19 @@ constexpr float INTERSECTION_CORRECTION = 0.00001f;   // MC/WhittedUtilities.h:1
 // Frozen stream (oracle/philox.h restates it independently): Philox4x32-10, key = seed,
 // counter = (pixel, frame, dim >> 2, 0), u32 = out[dim & 3], Float = (float)u / (float)UINT32_MAX
 // (Walnut::Random::Float, WN/Random.h:27-30).
+#ifndef RT_PHILOX_KEY_BARRIER
+#define RT_PHILOX_KEY_BARRIER 1
+#endif
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t out[4])
 {
     // each 32 x 32 -> 64-bit product as ONE v_mad_u64_u32 (the split __umulhi + low multiply is two
     // quarter-rate instructions)
+#if RT_PHILOX_KEY_BARRIER
+    // the key (uniform) through an opaque scalar move: the ten round keys are then formed here with scalar adds
+    // instead of being hoisted out of the kernel's loop as loop invariants, where the path kernels kept them
+    // in spilled SGPRs and read every one back with a v_readlane (a VALU slot and a hazard nop per round key)
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
