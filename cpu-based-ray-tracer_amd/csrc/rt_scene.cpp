@@ -68,7 +68,9 @@ inline float half_area(const Box& b)
     return ex * ey + ey * ez + ez * ex;
 }
 
-int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leaves, size_t lo, size_t hi)
+constexpr int kMaxSahBins = 1024;
+
+int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leaves, size_t lo, size_t hi, const int kBins)
 {
     const int me = (int)nodes.size();
     nodes.emplace_back();
@@ -86,7 +88,6 @@ int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leave
     int best_ax = -1;
     float best_split = 0.0f;
     size_t best_k = 0;   // exact sweep: the first best_k leaves (sorted on best_ax) go left
-    constexpr int kBins = 16;
     for (int a = 0; a < 3; ++a) {
         if (!(ch[a] > cl[a])) continue;
         if (n <= 2 * kBins) {   // small nodes: every split of the sorted order
@@ -105,9 +106,9 @@ int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leave
             }
             continue;
         }
-        Box bb[kBins];
-        size_t cnt[kBins] = {};
-        bool used[kBins] = {};
+        Box bb[kMaxSahBins];
+        size_t cnt[kMaxSahBins] = {};
+        bool used[kMaxSahBins] = {};
         const float scale = (float)kBins / (ch[a] - cl[a]);
         for (size_t i = lo; i < hi; ++i) {
             int k = (int)((cen(leaves[i].first, a) - cl[a]) * scale);
@@ -116,8 +117,8 @@ int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leave
             used[k] = true;
             ++cnt[k];
         }
-        float rarea[kBins];
-        size_t rcnt[kBins];
+        float rarea[kMaxSahBins];
+        size_t rcnt[kMaxSahBins];
         { Box rb{}; bool any = false; size_t c = 0;
           for (int k = kBins - 1; k >= 1; --k) {
               if (used[k]) { rb = any ? box_union(rb, bb[k]) : bb[k]; any = true; }
@@ -154,8 +155,8 @@ int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leave
         mid = (size_t)(it - leaves.begin());
         if (mid == lo || mid == hi) mid = lo + n / 2;
     }
-    const int l = build_sah(nodes, leaves, lo, mid);
-    const int r = build_sah(nodes, leaves, mid, hi);
+    const int l = build_sah(nodes, leaves, lo, mid, kBins);
+    const int r = build_sah(nodes, leaves, mid, hi, kBins);
     nodes[me].left = l; nodes[me].right = r;
     nodes[me].size = 1 + nodes[l].size + nodes[r].size;
     return me;
@@ -379,6 +380,9 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     // subtree (A/B knob RT_WALK_TREE)
     bool walk_tree_sah = true;
     if (const char* e = rt_knob("RT_WALK_TREE")) walk_tree_sah = std::strtol(e, nullptr, 10) != 0;
+    // bins per axis of the SAH build (A/B knob RT_SAH_BINS)
+    int sah_bins = 16;
+    if (const char* e = rt_knob("RT_SAH_BINS")) sah_bins = std::min(std::max((int)std::strtol(e, nullptr, 10), 2), kMaxSahBins);
     const size_t nm = meshes_.size();
     for (const auto& e : world_) {
         if (e.kind == 0 && !(e.radius > 0.0f)) { err = "world sphere with a non-positive radius"; return false; }
@@ -571,7 +575,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             for (uint32_t i = r; i < rend; ++i)
                 if (fn[i].tri >= 0) leaves.emplace_back(fn[i].box, fn[i].tri);
             tn.reserve(2 * leaves.size());
-            troot = build_sah(tn, leaves, 0, leaves.size());
+            troot = build_sah(tn, leaves, 0, leaves.size(), sah_bins);
         } else {
             tn.resize(M);
             for (uint32_t i = r; i < rend; ++i) {

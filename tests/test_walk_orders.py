@@ -152,3 +152,17 @@ def test_whitted_orders_of_c3(walk_tree, monkeypatch):
     sc = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"])
     assert sc.walk_orders() is None   # no split: the path tracer's vertex kernel does not walk this scene
     check_orders(sc, n_rays=30, seed=3, same_tree=walk_tree == "0", whitted=True)
+
+
+@pytest.mark.parametrize("bins", ["2", "1024"])
+def test_sah_bins_build_other_trees(bins, monkeypatch):
+    """RT_SAH_BINS (the A/B knob of the SAH build's bins per axis) builds another tree over the same leaves: its
+    orderings differ from the default 16-bin tree's and still give the reference's leaf set for every ray
+    (test_walk_variants_gpu.py renders with them)."""
+    z = np.load(SA.A.__file__.replace("test_skip_adversarial.py", "golden/bvh_scene.npz"))
+    base = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"]).walk_orders(whitted=True)
+    monkeypatch.setenv("RT_SAH_BINS", bins)
+    sc = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"])
+    other = sc.walk_orders(whitted=True)
+    assert other.shape == base.shape and not np.array_equal(other, base)
+    check_orders(sc, n_rays=20, seed=4, same_tree=False, whitted=True)

@@ -4,8 +4,10 @@ triangle) and a leaf box's own slab test decides whether the reference reaches i
 DESIGN.md 5.1 / 5.3).  Each variant builds its scene under its knobs (RT_WALK_TREE is read at the scene build)
 and renders bitwise against the reference's fixtures:
   * C3 (Whitted, bunny + teapot) at its full 1280x960x64 with the product kernel (no work counters): the SAH
-    tree's orderings (default), the reference tree's orderings (RT_WALK_TREE=0), the DFS walk (RT_WH_ORDER=0);
-  * C5 at 96x54x16 on the BVH variant with the reference tree's orderings (RT_WALK_TREE=0)."""
+    tree's orderings (default), the reference tree's orderings (RT_WALK_TREE=0), the DFS walk (RT_WH_ORDER=0),
+    SAH trees binned 2 and 1024 ways (RT_SAH_BINS: other trees over the same leaves);
+  * C5 at 96x54x16 on the BVH variant with the reference tree's orderings (RT_WALK_TREE=0) and the 2- and
+    1024-bin SAH trees."""
 import hashlib
 import os
 
@@ -22,7 +24,8 @@ def bits(a):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"RT_WALK_TREE": "0"}, {"RT_WH_ORDER": "0"}], ids=["sah-orders", "reference-tree-orders", "dfs"])
+@pytest.mark.parametrize("env", [{}, {"RT_WALK_TREE": "0"}, {"RT_WH_ORDER": "0"}, {"RT_SAH_BINS": "2"}, {"RT_SAH_BINS": "1024"}],
+                         ids=["sah-orders", "reference-tree-orders", "dfs", "sah-2-bins", "sah-1024-bins"])
 def test_c3_full_frame_product_kernel(env, monkeypatch):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -43,8 +46,11 @@ def test_c3_full_frame_product_kernel(env, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_c5_reference_tree_orders(monkeypatch):
-    monkeypatch.setenv("RT_WALK_TREE", "0")
+@pytest.mark.parametrize("env", [{"RT_WALK_TREE": "0"}, {"RT_SAH_BINS": "2"}, {"RT_SAH_BINS": "1024"}],
+                         ids=["reference-tree-orders", "sah-2-bins", "sah-1024-bins"])
+def test_c5_tree_variants(env, monkeypatch):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     bunny = np.load(os.path.join(G, "bvh_scene.npz"))["raw_bunny"]
     sc = rt.Scene.cornell_c5(bunny)
     c = rt.Context(0)

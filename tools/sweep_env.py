@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from _rt import rt  # noqa: E402
 
-KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_BVH_PREPASS", "RT_PRE_DEFER", "RT_WALK_TREE", "RT_SKY_BITS")
+KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_BVH_PREPASS", "RT_PRE_DEFER", "RT_WALK_TREE", "RT_SKY_BITS", "RT_SAH_BINS")
 
 
 def main():
@@ -31,14 +31,15 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--nranks", type=int, default=1)
     ap.add_argument("--fast", action="store_true")
-    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5"])
+    ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3"])
     ap.add_argument("--lib", default=None, help="library file in the package directory (default librt_hip.so)")
     args = ap.parse_args()
     if args.lib:
         rt.LIB_PATH = os.path.join(REPO, "cpu-based-ray-tracer_amd", args.lib)
     W, H, spp = args.width, args.height, args.spp
-    bunny = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))["raw_bunny"] if args.scene == "c5" else None
-    cam, _, _ = rt.camera_default(W, H)
+    bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz")) if args.scene in ("c5", "c3") else None
+    cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else rt.camera_default(W, H)[0]
+    kw = dict(whitted=True) if args.scene == "c3" else dict(exact=not args.fast)
     variants = args.set or [""]
     ctxs = []
     for v in variants:
@@ -48,14 +49,15 @@ def main():
             k, val = a.split("=")
             os.environ[k] = val
         # the scene is built under the variant's knobs too (RT_WALK_TREE is read by the scene build)
-        scene = rt.Scene.cornell_c5(bunny) if args.scene == "c5" else rt.Scene.cornell()
+        scene = (rt.Scene.cornell_c5(bvh["raw_bunny"]) if args.scene == "c5" else
+                 rt.Scene.bvh_tracer(bvh["raw_bunny"], bvh["raw_teapot"]) if args.scene == "c3" else rt.Scene.cornell())
         c = rt.Context(0)
         c.upload(scene)
         c.resize(W, H, 8, args.rank, args.nranks)
         ctxs.append((v, c, []))
     for r in range(args.rounds + 1):
         for v, c, res in ctxs:
-            c.render(cam, spp, fetch=False, exact=not args.fast)
+            c.render(cam, spp, fetch=False, **kw)
             if r > 0:
                 res.append(c.stats().last_kernel_ms)
     for v, c, res in ctxs:
