@@ -31,3 +31,19 @@ def test_knobs_read_with_the_gate(monkeypatch):
     monkeypatch.setenv("RT_DEBUG_KNOBS", "1")
     monkeypatch.setenv("RT_VERTEX", "0")
     assert render_kernel() == 0                   # RT_KERNEL_MEGA
+
+
+def test_scene_knobs_ignored_without_the_gate(monkeypatch):
+    """The scene build's knobs (RT_WALK_TREE, RT_SAH_BINS) too: without the gate the near-first orderings are
+    the default SAH tree's whatever the variables say (host code only, no GPU)."""
+    import os
+    import numpy as np
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bvh_scene.npz"))
+    monkeypatch.setenv("RT_DEBUG_KNOBS", "1")
+    base = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"]).walk_orders(whitted=True)
+    monkeypatch.setenv("RT_SAH_BINS", "2")
+    monkeypatch.setenv("RT_WALK_TREE", "0")
+    bits = lambda a: np.ascontiguousarray(a).view(np.uint32)   # (the orderings hold NaN fields: compare bits)
+    assert not np.array_equal(bits(rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"]).walk_orders(whitted=True)), bits(base))
+    monkeypatch.delenv("RT_DEBUG_KNOBS")
+    assert np.array_equal(bits(rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"]).walk_orders(whitted=True)), bits(base))
