@@ -119,6 +119,8 @@ struct rt_ctx {
     bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
     bool wh_order = true;     // Whitted kernel: walk the whole tree's near-first ordering of the ray's octant (RT_WH_ORDER=0: DFS)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
+    uint32_t seg_min_parts = 128; // A/B (RT_SEG_MIN_PARTS): path-kernel parts per wave the split aims for
+    uint32_t seg_part_lf = 4;     // A/B (RT_SEG_PART_LF): log2 of the fewest frames' worth of records in a part
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
@@ -457,6 +459,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WH_ORDER")) c->wh_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_SEG_MIN_PARTS")) c->seg_min_parts = (uint32_t)std::max(1ul, std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_SEG_PART_LF")) c->seg_part_lf = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
@@ -951,16 +955,19 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     Q.n_tiles = P.tiles_x * ((c->local_rows + 7) / 8);
                     uint32_t lf = 0;
                     while ((1u << lf) < nf && lf < 6) ++lf;
-                    // a wave of the path kernel takes parts of segments: keep at least 32 parts per wave, so
-                    // the launch's tail (the waves' last parts) stays short when a pass has few tiles (a rank's
+                    // a wave of the path kernel takes parts of segments: aim at 128 parts per wave, so the
+                    // launch's tail (the waves' last parts) stays short, also when a pass has few tiles (a rank's
                     // row bands of a multi-GPU frame).  The segments stay long (the pre-pass's per-segment
                     // work -- the tile's box list, the record counter -- is paid once per 64 frames) and the
-                    // path kernel splits each into 2^ps parts of its records, as fine as 8 frames' worth
-                    // (8 ranks at C4: 8 parts of 64-frame segments; one-segment-per-part with 8-frame
-                    // segments cost the pre-pass 0.9 ms more, profiles/r03/numbers/band_split*.jsonl)
+                    // path kernel splits each into 2^ps parts of its records, as fine as 16 frames' worth (a
+                    // 64-frame segment in 4 parts whenever fewer than 128 per wave would remain: C4 at N = 1
+                    // and 2 -0.7 %, N = 4 and 8 and C5 unchanged against round 4's rule of 32 parts per wave
+                    // as fine as 8 frames, profiles/r05/ab/ab_seg_parts_*.jsonl; 8-frame parts cost more per
+                    // part than the shorter tail saves; one-segment-per-part with 8-frame segments cost the
+                    // pre-pass 0.9 ms more, profiles/r03/numbers/band_split*.jsonl)
                     const uint64_t waves = (uint64_t)grid * (c->block / 64u);
                     uint32_t ps = 0;
-                    while (lf - ps > 3 && ((uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) << ps) < 32u * waves) ++ps;
+                    while (lf > ps + c->seg_part_lf && ((uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) << ps) < (uint64_t)c->seg_min_parts * waves) ++ps;
                     if (c->seg_parts_off) { lf -= ps; ps = 0; }   // A/B: short segments, one part each
                     Q.seg_part_shift = ps;
                     Q.seg_frames = 1u << lf;

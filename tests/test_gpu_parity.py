@@ -230,6 +230,21 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
         c.close()
     monkeypatch.delenv("RT_SEG_PARTS_OFF")
     assert np.array_equal(bits(v8), bits(v))
+    # parts as fine as one frame's worth of records (RT_SEG_PART_LF=0; 64 parts per segment) and as many
+    # as the split allows (RT_SEG_MIN_PARTS): the same bits
+    monkeypatch.setenv("RT_SEG_MIN_PARTS", "100000")
+    monkeypatch.setenv("RT_SEG_PART_LF", "0")
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        _, v1 = c.render(cam, 70, seed=3)
+        assert c.stats().kernel == 1 and c.stats().n_chunks == 2
+    finally:
+        c.close()
+    monkeypatch.delenv("RT_SEG_MIN_PARTS")
+    monkeypatch.delenv("RT_SEG_PART_LF")
+    assert np.array_equal(bits(v1), bits(v))
     monkeypatch.setenv("RT_VERTEX", "0")
     c = rt.Context(0)
     try:
