@@ -208,9 +208,9 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
     monkeypatch.delenv("RT_VERTEX")
     monkeypatch.delenv("RT_CHUNKS")
     # the vertex kernel: its camera pre-pass groups a tile's frames in segments of up to 64 frames (70
-    # frames: 2 segments per tile, the last of 6), and the path kernel takes each segment in up to 8 parts
-    # when a pass has few tiles (here 8).  RT_SEG_PARTS_OFF=1 shortens the segments instead (8 frames: 9
-    # segments per tile, the last of 6, one part each); both give the megakernel's bits
+    # frames: 2 segments per tile, the last of 6), and the path kernel takes each segment in up to 4 parts
+    # (16 frames' worth) when a pass has few tiles (here 8).  RT_SEG_PARTS_OFF=1 shortens the segments instead
+    # (16 frames: 5 segments per tile, the last of 6, one part each); both give the megakernel's bits
     c = rt.Context(0)
     try:
         c.upload(rt.Scene.cornell())
@@ -225,7 +225,7 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
         c.upload(rt.Scene.cornell())
         c.resize(W, H)
         _, v8 = c.render(cam, 70, seed=3)
-        assert c.stats().kernel == 1 and c.stats().n_chunks == 9
+        assert c.stats().kernel == 1 and c.stats().n_chunks == 5
     finally:
         c.close()
     monkeypatch.delenv("RT_SEG_PARTS_OFF")
