@@ -512,6 +512,10 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
 #if RT_SECTIONS
     uint64_t sec_cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t sec_t = clock64();
+    // the launch's timeline in the chip-wide 100 MHz clock (wall_clock64): the wave's entry, the moment its
+    // work queue ran dry, its exit -> counters[440..447] (tools/prof_one.py --sections prints the tail)
+    const uint64_t tl_entry = wall_clock64();
+    uint64_t tl_empty = 0;
     int sec_cur = 7;
 #define SEC_MARK(k) do { const uint64_t t_ = clock64(); sec_cyc[sec_cur] += t_ - sec_t; sec_t = t_; sec_cur = (k); } while (0)
     // wave-level event counts in the wave's LDS slot (RT_SEC_COUNTS words, written by the wave's first
@@ -543,7 +547,13 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
                 k = __builtin_amdgcn_readfirstlane(k);
                 // (the list length is read here, once per segment, not kept live across the loop)
-                if (k >= (__builtin_amdgcn_readfirstlane(*Q.seg_list_n) << Q.seg_part_shift)) { list_left = false; break; }
+                if (k >= (__builtin_amdgcn_readfirstlane(*Q.seg_list_n) << Q.seg_part_shift)) {
+                    list_left = false;
+#if RT_SECTIONS
+                    tl_empty = wall_clock64();
+#endif
+                    break;
+                }
                 // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records
                 const uint32_t ps = Q.seg_part_shift, part = k & ((1u << ps) - 1u);
                 const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k >> ps]);
@@ -1389,6 +1399,17 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long*)&P.counters[16 + i], (unsigned long long)sec_cyc[i]);
     // the wave's event counts -> counters[24 + i]
     if (lane < RT_SEC_COUNTS) atomicAdd((unsigned long long*)&P.counters[24 + lane], (unsigned long long)sec_w[lane]);
+    if (__lane_id() == 0) {
+        // [440] ~first entry, [441] last entry, [442] ~first dry queue, [443] last dry queue, [444] last exit,
+        // [445] sum over waves of exit - dry queue, [446] waves, [447] sum of dry queue - entry (100 MHz ticks)
+        const uint64_t tl_exit = wall_clock64();
+        const uint64_t em = tl_empty != 0 ? tl_empty : tl_exit;
+        unsigned long long* tc = (unsigned long long*)P.counters;
+        atomicMax(&tc[440], (unsigned long long)~tl_entry); atomicMax(&tc[441], (unsigned long long)tl_entry);
+        atomicMax(&tc[442], (unsigned long long)~em); atomicMax(&tc[443], (unsigned long long)em);
+        atomicMax(&tc[444], (unsigned long long)tl_exit);
+        atomicAdd(&tc[445], (unsigned long long)(tl_exit - em)); atomicAdd(&tc[446], 1ull); atomicAdd(&tc[447], (unsigned long long)(em - tl_entry));
+    }
 #endif
 }
 

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3"])
     ap.add_argument("--hist", action="store_true", help="print the candidate histograms of an RT_SECTIONS=3 build")
     ap.add_argument("--reps", type=int, default=1, help="measured renders after the warm-up")
+    ap.add_argument("--nranks", type=int, default=1, help="render rank --rank's row bands of an N-rank frame")
+    ap.add_argument("--rank", type=int, default=0)
     args = ap.parse_args()
     spec = importlib.util.spec_from_file_location("rt_amd", os.path.join(PKG, "__init__.py"))
     rt = importlib.util.module_from_spec(spec)
@@ -43,12 +45,12 @@ def main():
         kw = dict(whitted=True)
     else:
         c.upload(rt.Scene.cornell())
-    c.resize(args.width, args.height)
+    c.resize(args.width, args.height, 8, args.rank, args.nranks)
     cam = rt.camera_bvh_tracer(args.width, args.height) if args.scene == "c3" else rt.camera_default(args.width, args.height)[0]
     for _ in range(1 + args.reps):
         c.render(cam, args.spp, fetch=False, **kw)
     st = c.stats()
-    print(f"{args.lib}: {st.last_kernel_ms:.2f} ms, {args.width * args.height * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
+    print(f"{args.lib}: {st.last_kernel_ms:.2f} ms (path kernel {st.last_main_ms:.2f}), {c.local_rows * args.width * args.spp / st.last_kernel_ms / 1e3:.1f} Msamples/s")
     if args.sections:
         cyc = c.debug_counters(24)[16:24]
         # rt_coherent.hip SEC_MARK: [0] top (path ends, fold drain, work / camera records), [1] path end (fold set-up,
@@ -59,7 +61,7 @@ def main():
         print({n: round(v / tot, 4) for n, v in zip(names, cyc)})
         n = c.debug_counters(44)[24:44]
         it = max(n[0], 1)
-        samples = args.width * args.height * args.spp
+        samples = c.local_rows * args.width * args.spp
         print({"wave_iterations": n[0], "lanes_on_path/it": round(n[1] / it, 2), "vertex/it": round(n[2] / it, 2),
                "finish/it": round(n[3] / it, 2), "camera/it": round(n[4] / it, 2),
                "mt_iters/it": round(n[5] / it, 2), "mt_lane_util": round(n[6] / max(n[5], 1) / 64, 3),
@@ -69,6 +71,18 @@ def main():
                "drain_lanes_top/it": round(n[11] / it, 2),
                "union_tris_A/it": round(n[16] / it, 2), "union_tris_B/it": round(n[17] / it, 2), "union_tris_AB/it": round(n[18] / it, 2), "mt_open/it": round(n[19] / it, 4),
                "lane_iterations_per_sample": round(n[0] * 64 / samples, 3)})
+    if args.sections and not args.hist:
+        # the launch's timeline (rt_coherent.hip, RT_SECTIONS builds; wall_clock64 ticks at 100 MHz): how long the
+        # waves run after their work queue ran dry (the launch's tail) -- meaningful for one render (--reps 0)
+        t = c.debug_counters(448)[440:448]
+        inv = lambda v: (~v) & 0xFFFFFFFFFFFFFFFF
+        first_entry, last_entry, first_dry, last_dry, last_exit = inv(t[0]), t[1], inv(t[2]), t[3], t[4]
+        waves = max(t[6], 1)
+        ms = lambda ticks: round(ticks / 1e5, 3)
+        print(json.dumps({"timeline_ms": {"entry_spread": ms(last_entry - first_entry), "first_dry_queue": ms(first_dry - first_entry),
+                                          "last_dry_queue": ms(last_dry - first_entry), "last_exit": ms(last_exit - first_entry),
+                                          "mean_wave_tail_after_dry_queue": ms(t[5] / waves), "mean_wave_busy_until_dry": ms(t[7] / waves)},
+                          "waves": t[6], "reps": args.reps}))
     if args.hist:
         h = c.debug_counters(512)
         tot = lambda a, b: sum(h[a:b])
