@@ -121,6 +121,8 @@ struct rt_ctx {
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     uint32_t seg_min_parts = 128; // A/B (RT_SEG_MIN_PARTS): path-kernel parts per wave the split aims for
     uint32_t seg_part_lf = 4;     // A/B (RT_SEG_PART_LF): log2 of the fewest frames' worth of records in a part
+    uint32_t seg_tail_parts = 2;  // A/B (RT_SEG_TAIL_PARTS): each wave's last parts' worth of segments taken finer ...
+    uint32_t seg_tail_extra = 1;  // A/B (RT_SEG_TAIL_EXTRA): ... in 2^extra times as many parts (0: no tail split)
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
@@ -461,6 +463,8 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SEG_MIN_PARTS")) c->seg_min_parts = (uint32_t)std::max(1ul, std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_SEG_PART_LF")) c->seg_part_lf = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_SEG_TAIL_PARTS")) c->seg_tail_parts = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (const char* e = rt_knob("RT_SEG_TAIL_EXTRA")) c->seg_tail_extra = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
@@ -970,6 +974,10 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     while (lf > ps + c->seg_part_lf && ((uint64_t)Q.n_tiles * ((nf + (1u << lf) - 1u) >> lf) << ps) < (uint64_t)c->seg_min_parts * waves) ++ps;
                     if (c->seg_parts_off) { lf -= ps; ps = 0; }   // A/B: short segments, one part each
                     Q.seg_part_shift = ps;
+                    // the launch's tail: the list's last segments (each wave's last seg_tail_parts parts' worth)
+                    // in 2^seg_tail_extra times as many parts, no finer than one frame's worth of records
+                    Q.seg_tail_shift = std::min(ps + c->seg_tail_extra, lf);
+                    Q.seg_tail_n = (uint32_t)std::min<uint64_t>(((uint64_t)c->seg_tail_parts * waves) >> ps, 0xFFFFFFFFull);
                     Q.seg_frames = 1u << lf;
                     Q.seg_shift = 6 + lf;
                     const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);

@@ -547,19 +547,30 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
                 k = __builtin_amdgcn_readfirstlane(k);
                 // (the list length is read here, once per segment, not kept live across the loop)
-                if (k >= (__builtin_amdgcn_readfirstlane(*Q.seg_list_n) << Q.seg_part_shift)) {
-                    list_left = false;
+                // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records;
+                // the list's last seg_tail_n segments in 2^seg_tail_shift finer parts, so the waves run dry
+                // within a short part of each other at the end of the launch (the launch's tail)
+                const uint32_t nl = __builtin_amdgcn_readfirstlane(*Q.seg_list_n);
+                const uint32_t ps = Q.seg_part_shift, pt = Q.seg_tail_shift;
+                const uint32_t head = nl - (nl < Q.seg_tail_n ? nl : Q.seg_tail_n);
+                uint32_t idx, part, sh;
+                if (k < (head << ps)) {
+                    idx = k >> ps; part = k & ((1u << ps) - 1u); sh = ps;
+                } else {
+                    const uint32_t k2 = k - (head << ps);
+                    if (k2 >= ((nl - head) << pt)) {
+                        list_left = false;
 #if RT_SECTIONS
-                    tl_empty = wall_clock64();
+                        tl_empty = wall_clock64();
 #endif
-                    break;
+                        break;
+                    }
+                    idx = head + (k2 >> pt); part = k2 & ((1u << pt) - 1u); sh = pt;
                 }
-                // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records
-                const uint32_t ps = Q.seg_part_shift, part = k & ((1u << ps) - 1u);
-                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[k >> ps]);
+                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[idx]);
                 const uint32_t cnt = __builtin_amdgcn_readfirstlane(Q.ccount[sg]);
-                seg_pos = (sg << Q.seg_shift) + ((part * cnt) >> ps);
-                seg_end = (sg << Q.seg_shift) + (((part + 1u) * cnt) >> ps);
+                seg_pos = (sg << Q.seg_shift) + ((part * cnt) >> sh);
+                seg_end = (sg << Q.seg_shift) + (((part + 1u) * cnt) >> sh);
                 continue;
             }
             const uint32_t avail = seg_end - seg_pos;
@@ -1742,6 +1753,10 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
     if (lane == 0) {
         P.ccount[sg] = cnt;
         if (cnt != 0u) P.seg_list[atomicAdd(P.seg_list_n, 1u)] = sg;
+#if RT_SECTIONS
+        // (diagnostic) segments by record count, 256-record bins -> counters[448 + bin] (tools/prof_one.py)
+        atomicAdd((unsigned long long*)&P.counters[448 + min(cnt >> 8, 16u)], 1ull);
+#endif
     }
 }
 

@@ -93,6 +93,9 @@ struct KParams {
     // instead of walked here (0: the pre-pass walks it)
     uint32_t pre_defer_walk;
     uint32_t n_segments, n_tiles, seg_frames, seg_shift, seg_part_shift;
+    // ... and the list's last seg_tail_n segments in 2^seg_tail_shift parts (>= seg_part_shift; finer work at the
+    // launch's end)
+    uint32_t seg_tail_n, seg_tail_shift;
     uint32_t thresh;                // serve finished lanes once at most `thresh` lanes of a wave still trace
     uint32_t steps;                 // box tests per lane per traversal round (a parked leaf ends a round early)
     uint32_t force_walk;            // diagnostic (RT_FORCE_WALK): the vertex kernel walks the BVH for every ray
