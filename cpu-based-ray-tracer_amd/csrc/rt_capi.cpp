@@ -105,7 +105,7 @@ struct rt_ctx {
     // the vertex kernel's camera pre-pass: surface-hit records, per-segment counts, the non-empty segments
     float4* d_crec = nullptr;
     size_t crec_quads = 0;
-    uint32_t *d_ccount = nullptr, *d_seg_list = nullptr;
+    uint2* d_seg_list = nullptr;
     size_t seg_words = 0;
     unsigned long long* d_tile_boxes = nullptr;   // the pre-pass's per-tile leaf-box masks
     size_t tile_words = 0;
@@ -536,7 +536,7 @@ void rt_destroy(rt_ctx* c)
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
     dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf); dfree(c->d_sky);
-    dfree(c->d_crec); dfree(c->d_ccount); dfree(c->d_seg_list); dfree(c->d_tile_boxes);
+    dfree(c->d_crec); dfree(c->d_seg_list); dfree(c->d_tile_boxes);
     if (c->ev2) (void)hipEventDestroy(c->ev2);
     if (c->ev3) (void)hipEventDestroy(c->ev3);
     dfree(c->d_accum); dfree(c->d_rgba); dfree(c->d_counter); dfree(c->d_counters); dfree(c->d_stack_ld); dfree(c->d_stack_mat);
@@ -999,10 +999,9 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     }
                     if (nseg > c->seg_words) {
                         HIPC(c, hipStreamSynchronize(c->stream));
-                        dfree(c->d_ccount); dfree(c->d_seg_list);
+                        dfree(c->d_seg_list);
                         c->seg_words = 0;
-                        HIPC(c, hipMalloc((void**)&c->d_ccount, (size_t)nseg * 4));
-                        HIPC(c, hipMalloc((void**)&c->d_seg_list, (size_t)nseg * 4));
+                        HIPC(c, hipMalloc((void**)&c->d_seg_list, (size_t)nseg * sizeof(uint2)));
                         c->seg_words = (size_t)nseg;
                     }
                     if (Q.n_tiles > c->tile_words) {
@@ -1027,7 +1026,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                         }
                         Q.sky_bits = c->d_sky; Q.sky_words = sw;
                     }
-                    Q.crec = c->d_crec; Q.ccount = c->d_ccount; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
+                    Q.crec = c->d_crec; Q.seg_list = c->d_seg_list; Q.seg_list_n = c->d_counter + 1;
                     Q.tile_boxes = c->d_tile_boxes;
                     Q.n_chunks = (uint32_t)(nseg / Q.n_tiles);
                     const size_t pre_lds = coh_bvh ? (size_t)3 * P.n_split_leaves * sizeof(float4) : (size_t)(4 * P.n_tris + 2 * P.n_mats) * sizeof(float4);

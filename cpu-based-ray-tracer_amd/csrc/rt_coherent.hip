@@ -567,8 +567,9 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     }
                     idx = head + (k2 >> pt); part = k2 & ((1u << pt) - 1u); sh = pt;
                 }
-                const uint32_t sg = __builtin_amdgcn_readfirstlane(Q.seg_list[idx]);
-                const uint32_t cnt = __builtin_amdgcn_readfirstlane(Q.ccount[sg]);
+                const uint2 ent = Q.seg_list[idx];   // (segment, record count)
+                const uint32_t sg = __builtin_amdgcn_readfirstlane(ent.x);
+                const uint32_t cnt = __builtin_amdgcn_readfirstlane(ent.y);
                 seg_pos = (sg << Q.seg_shift) + ((part * cnt) >> sh);
                 seg_end = (sg << Q.seg_shift) + (((part + 1u) * cnt) >> sh);
                 continue;
@@ -1751,8 +1752,7 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
         if (nf > 32u) P.sky_bits[(size_t)(w0 + 1u) * px + local] = (uint32_t)(skym >> 32);
     }
     if (lane == 0) {
-        P.ccount[sg] = cnt;
-        if (cnt != 0u) P.seg_list[atomicAdd(P.seg_list_n, 1u)] = sg;
+        if (cnt != 0u) P.seg_list[atomicAdd(P.seg_list_n, 1u)] = make_uint2(sg, cnt);
 #if RT_SECTIONS
         // (diagnostic) segments by record count, 256-record bins -> counters[448 + bin] (tools/prof_one.py)
         atomicAdd((unsigned long long*)&P.counters[448 + min(cnt >> 8, 16u)], 1ull);

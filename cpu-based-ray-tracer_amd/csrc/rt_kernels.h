@@ -81,12 +81,13 @@ struct KParams {
     uint32_t lds_scene_quads;       // float4s of LDS taken by the staged scene (0 when the scene is in HBM)
     // the vertex kernel's camera pre-pass (camera_prepass_kernel, rt_coherent.hip): samples in segments of one
     // 8x8 tile x seg_frames (a power of two <= 64) frames, segment s = chunk * n_tiles + tile (chunk-major);
-    // the surface hits of segment s are records [s << seg_shift, + ccount[s]) of crec: (location.xyz, tag),
+    // the surface hits of segment s are records [s << seg_shift, + its record count) of crec: (location.xyz, tag),
     // tag = triangle | pixel-in-tile << 19 | frame-in-chunk << 25 | flipped normal << 31; the non-empty
     // segments are listed in seg_list[0, *seg_list_n) (misses and light hits are parked by the pre-pass);
     // the path kernel takes each listed segment in 2^seg_part_shift parts (consecutive record ranges), so a
-    // pass with few tiles keeps long pre-pass segments and still hands out fine-grained work
-    float4* crec; uint32_t* ccount; uint32_t* seg_list; uint32_t* seg_list_n;
+    // pass with few tiles keeps long pre-pass segments and still hands out fine-grained work; a list entry is
+    // (segment, its record count), so a wave's work fetch is the counter's atomic and one 8-byte load
+    float4* crec; uint2* seg_list; uint32_t* seg_list_n;
     unsigned long long* tile_boxes;   // per tile: the leaf boxes its camera rays' frustum meets (tile_boxes_kernel)
     // split scenes (the BVH variant's pre-pass): a camera ray that enters the walked subtree's box is recorded as a
     // camera ray (triangle field CREC_CAMERA, its direction in the location's place) and traced by the path kernel,

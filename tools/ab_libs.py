@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--scene", default="cornell", choices=["cornell", "c5", "c3", "c1"])
+    ap.add_argument("--nranks", type=int, default=1, help="render rank --rank's row bands of an N-rank frame")
+    ap.add_argument("--rank", type=int, default=0)
     args = ap.parse_args()
     W, H, spp = args.width, args.height, args.spp
     runs = {}
@@ -55,7 +57,7 @@ def main():
             sc = rt.Scene.cornell()
         ctx = rt.Context(0)
         ctx.upload(sc)
-        ctx.resize(W, H)
+        ctx.resize(W, H, 8, args.rank, args.nranks)
         cam = rt.camera_bvh_tracer(W, H) if args.scene == "c3" else (rt.camera_two_spheres(W, H) if args.scene == "c1" else rt.camera_default(W, H)[0])
         for k, _ in kv:
             os.environ.pop(k, None)
@@ -67,7 +69,7 @@ def main():
             ctx.render(cam, spp, fetch=False, **kw)
             if r > 0:
                 st = ctx.stats()
-                res.append(W * H * spp / st.last_kernel_ms / 1e3)
+                res.append(ctx.local_rows * W * spp / st.last_kernel_ms / 1e3)
                 pre.append(st.last_prepass_ms)
                 main.append(st.last_main_ms)
     out = {}
@@ -78,7 +80,7 @@ def main():
         out[name] = {"median_msps": round(float(np.median(res)), 1), "grid": ctx.stats().grid, "bitwise_equal_to_first": same,
                      "prepass_ms": round(float(np.median(pre)), 3), "path_kernel_ms": round(float(np.median(main)), 3)}
         ctx.close()
-    print(json.dumps({"config": f"{W}x{H}x{spp} {args.scene} {'fast' if args.fast else 'exact'}", "libs": out}, indent=1))
+    print(json.dumps({"config": f"{W}x{H}x{spp} {args.scene} {'fast' if args.fast else 'exact'}", "rank": args.rank, "nranks": args.nranks, "libs": out}, indent=1))
 
 
 if __name__ == "__main__":
