@@ -25,6 +25,9 @@ struct rt_scene {
 // device counters: [0, 64) work / overflow / section counters, [64, 512) diagnostic histograms
 // (RT_SECTIONS >= 3 builds, rt_coherent.hip)
 static constexpr uint32_t kCounterWords = 512;
+// the work counters: [0] items / parts (one queue), [1] the pre-pass's list length, and from word 32 the path
+// kernel's 8 part queues, 32 words (128 B) apart
+static constexpr size_t kWorkCounterBytes = (32 + 8 * 32) * sizeof(uint32_t);
 
 struct rt_ctx {
     int device = 0;
@@ -121,8 +124,9 @@ struct rt_ctx {
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     uint32_t seg_min_parts = 128; // A/B (RT_SEG_MIN_PARTS): path-kernel parts per wave the split aims for
     uint32_t seg_part_lf = 4;     // A/B (RT_SEG_PART_LF): log2 of the fewest frames' worth of records in a part
-    uint32_t seg_tail_parts = 2;  // A/B (RT_SEG_TAIL_PARTS): each wave's last parts' worth of segments taken finer ...
-    uint32_t seg_tail_extra = 1;  // A/B (RT_SEG_TAIL_EXTRA): ... in 2^extra times as many parts (0: no tail split)
+    uint32_t seg_tail_parts = 8;  // A/B (RT_SEG_TAIL_PARTS): each wave's last parts' worth of segments taken finer ...
+    uint32_t seg_tail_extra = 3;  // A/B (RT_SEG_TAIL_EXTRA): ... in 2^extra times as many parts (0: no tail split)
+    uint32_t n_work_queues = 8;   // A/B (RT_WORK_QUEUES, 1 or 8): counters handing out the path kernel's parts
     bool vertex_bvh = true;   // other scenes: the vertex kernel's BVH variant (RT_VERTEX_BVH=0: the megakernel)
     uint32_t lds_pad = 0;   // diagnostic: extra dynamic LDS bytes per workgroup (RT_LDS_PAD) to lower occupancy
     uint32_t thresh = 8, steps = 12;   // traversal scheduling (tuned on MI355X, profiles/) (RT_THRESH / RT_STEPS override)
@@ -465,6 +469,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_SEG_PART_LF")) c->seg_part_lf = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_SEG_TAIL_PARTS")) c->seg_tail_parts = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_SEG_TAIL_EXTRA")) c->seg_tail_extra = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
+    if (const char* e = rt_knob("RT_WORK_QUEUES")) c->n_work_queues = std::strtoul(e, nullptr, 10) >= 8 ? 8u : 1u;
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
@@ -493,7 +498,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     }
     if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess || hipEventCreate(&c->ev2) != hipSuccess ||
         hipEventCreate(&c->ev3) != hipSuccess ||
-        hipMalloc((void**)&c->d_counter, 64) != hipSuccess || hipMalloc((void**)&c->d_counters, kCounterWords * 8) != hipSuccess ||
+        hipMalloc((void**)&c->d_counter, kWorkCounterBytes) != hipSuccess || hipMalloc((void**)&c->d_counters, kCounterWords * 8) != hipSuccess ||
         hipHostMalloc((void**)&c->h_ovf, 2 * sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
         c->err = "context allocation failed";
         rt_destroy(c);
@@ -782,6 +787,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     P.n_items = (uint32_t)items;
     P.accum = c->d_accum; P.rgba = c->d_rgba;
     P.work_counter = c->d_counter;
+    P.work_queues = c->d_counter + 32; P.n_work_queues = c->n_work_queues;
     P.stack_ld = c->d_stack_ld; P.stack_mat = c->d_stack_mat; P.stack_depth = exact ? c->stack_depth : 0;
     // read by the vertex kernel only; set below for its BVH variant (C5 198.6 vs 203.4 ms; the leaf-box
     // variant measured 0.6 % slower with it: C4 346.8 vs 344.5 ms)
@@ -946,7 +952,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     }
                     Q.lbuf = c->d_lbuf; Q.lbuf_stride = (size_t)px_local;
                 }
-                HIPC(c, hipMemsetAsync(c->d_counter, 0, 64, c->stream));
+                HIPC(c, hipMemsetAsync(c->d_counter, 0, kWorkCounterBytes, c->stream));
                 HIPC(c, hipMemsetAsync(c->d_counters + 3, 0, sizeof(unsigned long long), c->stream));   // this pass's overflow list
                 while (c->kev.size() < 3 * (size_t)(pass + 1)) {
                     hipEvent_t e = nullptr;

@@ -507,6 +507,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
     // the wave's current segment of camera-hit records (wave-uniform): records [seg_pos, seg_end) are not
     // yet taken; the non-empty segments are taken one per device atomic from the pre-pass's list
     uint32_t seg_pos = 0, seg_end = 0;
+    uint32_t wq = blockIdx.x & (P.n_work_queues - 1u), wq_dry = 0;   // the wave's work queue; queues found dry in a row
     bool list_left = true;
 
 #if RT_SECTIONS
@@ -544,8 +545,8 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 if (!list_left) break;
                 CKParams& Q = kargs4();
                 uint32_t k = 0;
-                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_counter, 1u);
-                k = __builtin_amdgcn_readfirstlane(k);
+                if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) k = atomicAdd(Q.work_queues + 32u * wq, 1u);
+                k = __builtin_amdgcn_readfirstlane(k) * Q.n_work_queues + wq;
                 // (the list length is read here, once per segment, not kept live across the loop)
                 // list entry k: part (k mod 2^ps) of listed segment k >> ps, a consecutive range of its records;
                 // the list's last seg_tail_n segments in 2^seg_tail_shift finer parts, so the waves run dry
@@ -559,6 +560,10 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 } else {
                     const uint32_t k2 = k - (head << ps);
                     if (k2 >= ((nl - head) << pt)) {
+                        // this queue is dry (for good: its draws only grow): the next one, until every queue
+                        // has been found dry in a row
+                        wq = (wq + 1u) & (Q.n_work_queues - 1u);
+                        if (++wq_dry < Q.n_work_queues) continue;
                         list_left = false;
 #if RT_SECTIONS
                         tl_empty = wall_clock64();
@@ -567,6 +572,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     }
                     idx = head + (k2 >> pt); part = k2 & ((1u << pt) - 1u); sh = pt;
                 }
+                wq_dry = 0;
                 const uint2 ent = Q.seg_list[idx];   // (segment, record count)
                 const uint32_t sg = __builtin_amdgcn_readfirstlane(ent.x);
                 const uint32_t cnt = __builtin_amdgcn_readfirstlane(ent.y);

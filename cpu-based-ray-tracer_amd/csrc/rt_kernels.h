@@ -71,6 +71,10 @@ struct KParams {
     float4* accum; uint32_t* rgba;
     // scratch
     uint32_t* work_counter;
+    // the vertex kernel's segment parts are handed out by n_work_queues counters (1 or 8), 32 words apart from
+    // work_queues: block b draws from queue b mod n (the XCD it runs on), part k = j * n + queue for its j-th
+    // draw, and moves to the next queue when its own is dry
+    uint32_t* work_queues; uint32_t n_work_queues;
     float4* stack_ld; int32_t* stack_mat; uint32_t stack_depth; uint32_t total_threads;
     // vertex kernel, EXACT: a scene of at most 8 materials keeps a fold level's material in the sign bits
     // of its direct term (always +0 or positive; a zero's sign never reaches the accumulation: the sums
