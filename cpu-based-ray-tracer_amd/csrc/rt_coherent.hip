@@ -1427,6 +1427,8 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         atomicMax(&tc[442], (unsigned long long)~em); atomicMax(&tc[443], (unsigned long long)em);
         atomicMax(&tc[444], (unsigned long long)tl_exit);
         atomicAdd(&tc[445], (unsigned long long)(tl_exit - em)); atomicAdd(&tc[446], 1ull); atomicAdd(&tc[447], (unsigned long long)(em - tl_entry));
+        // [466 + b] waves by their time from the dry queue to their exit, 0.1 ms bins (the last one open)
+        atomicAdd(&tc[466 + min((uint32_t)((tl_exit - em) / 10000u), 21u)], 1ull);
     }
 #endif
 }

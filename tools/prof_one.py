@@ -83,7 +83,8 @@ def main():
                                           "last_dry_queue": ms(last_dry - first_entry), "last_exit": ms(last_exit - first_entry),
                                           "mean_wave_tail_after_dry_queue": ms(t[5] / waves), "mean_wave_busy_until_dry": ms(t[7] / waves)},
                           "waves": t[6], "reps": args.reps,
-                          "segments_by_records_256": c.debug_counters(465)[448:465]}))
+                          "segments_by_records_256": c.debug_counters(465)[448:465],
+                          "waves_by_exit_minus_dry_0p1ms": c.debug_counters(488)[466:488]}))
     if args.hist:
         h = c.debug_counters(512)
         tot = lambda a, b: sum(h[a:b])
