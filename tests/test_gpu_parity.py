@@ -245,6 +245,20 @@ def test_frame_chunks_are_bitwise_neutral(monkeypatch):
     monkeypatch.delenv("RT_SEG_MIN_PARTS")
     monkeypatch.delenv("RT_SEG_PART_LF")
     assert np.array_equal(bits(v1), bits(v))
+    # one work queue and no finer tail (the default: 8 per-XCD queues, most of them dry at once on this small
+    # frame, and the list's last parts split 8x): the same bits
+    monkeypatch.setenv("RT_WORK_QUEUES", "1")
+    monkeypatch.setenv("RT_SEG_TAIL_EXTRA", "0")
+    c = rt.Context(0)
+    try:
+        c.upload(rt.Scene.cornell())
+        c.resize(W, H)
+        _, vq = c.render(cam, 70, seed=3)
+    finally:
+        c.close()
+    monkeypatch.delenv("RT_WORK_QUEUES")
+    monkeypatch.delenv("RT_SEG_TAIL_EXTRA")
+    assert np.array_equal(bits(vq), bits(v))
     monkeypatch.setenv("RT_VERTEX", "0")
     c = rt.Context(0)
     try:
