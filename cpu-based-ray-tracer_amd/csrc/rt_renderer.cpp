@@ -10,15 +10,47 @@
 
 namespace rt {
 
+// ============================================================================ layout guard (rt/Abi.h)
+namespace {
+const char* abi_class_name(AbiClass c)
+{
+    switch (c) {
+    case AbiClass::Renderer: return "rt::Renderer";
+    case AbiClass::Camera: return "rt::Camera";
+    case AbiClass::WhittedRenderer: return "rt::WhittedRenderer";
+    case AbiClass::DenoisingRenderer: return "rt::DenoisingRenderer";
+    }
+    return "rt class";
+}
+}  // namespace
+
+AbiGuard::AbiGuard(const AbiTag& caller, uint64_t lib_size, uint64_t lib_aux_size) : version_(RT_CXX_ABI_VERSION)
+{
+    // runs before any other member of the caller's object is written: nothing past this member is touched
+    // when it throws
+    if (caller.version != RT_CXX_ABI_VERSION || caller.size != lib_size || caller.aux_size != lib_aux_size)
+        throw rt::Error(std::string(abi_class_name(caller.cls)) + ": the caller was compiled against a different include/rt " +
+                        "header than librt_hip.so (C++ ABI " + std::to_string(caller.version) + " vs " +
+                        std::to_string(RT_CXX_ABI_VERSION) + ", sizeof " + std::to_string(caller.size) + " vs " +
+                        std::to_string(lib_size) + ", Settings " + std::to_string(caller.aux_size) + " vs " +
+                        std::to_string(lib_aux_size) + "); rebuild the front-end against this library's headers");
+    // the C structs too: the caller's RT_API_VERSION against the library's
+    if (rt_api_version() != RT_API_VERSION)
+        throw rt::Error("librt_hip.so C-ABI version " + std::to_string(rt_api_version()) + ", include/rt_capi.h " +
+                        std::to_string(RT_API_VERSION));
+}
+
 // ============================================================================ Camera
-Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance)
-    : vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance}, far_clip_plane_distance{FarClipPlaneDistance}
+Camera::Camera(const AbiTag& caller, float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance)
+    : abi_(caller, sizeof(Camera), 0), vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance},
+      far_clip_plane_distance{FarClipPlaneDistance}
 {
 }
 
-Camera::Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 p, rt::vec3 f)
-    : position{p}, forward_direction{f}, vertical_FOV{verticalFOV}, near_clip_plane_distance{NearClipPlaneDistance},
-      far_clip_plane_distance{FarClipPlaneDistance}
+Camera::Camera(const AbiTag& caller, float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 p,
+               rt::vec3 f)
+    : abi_(caller, sizeof(Camera), 0), position{p}, forward_direction{f}, vertical_FOV{verticalFOV},
+      near_clip_plane_distance{NearClipPlaneDistance}, far_clip_plane_distance{FarClipPlaneDistance}
 {
 }
 
@@ -161,23 +193,64 @@ rt::TriangleMesh::TriangleMesh(std::vector<float> raw_positions, const Material&
 // ============================================================================ Renderer
 namespace rt {
 
-void Renderer::check(rt_status s, const char* what) const
-{
-    if (s != RT_OK)
-        throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + (group ? rt_group_last_error(group) : rt_last_error(ctx)));
-}
+// the library's state behind rt::Renderer's one pointer (the caller allocates only the public members, the
+// guard and this pointer)
+struct Renderer::Impl {
+    Settings settings;
+    std::shared_ptr<rt::Image> frame_image_final;
+    std::vector<float> accum_host;
+    uint32_t frame_accumulating = 1;
+    uint64_t epoch = 0;
+    rt_ctx* ctx = nullptr;
+    rt_group* group = nullptr;   // Settings::devices with more than one entry
+    std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
+    rt_scene* scene = nullptr;
+    bool bvh_dirty = true;
+    // the queries' context: ctx, or (several devices) one on the first device holding the scene
+    rt_ctx* qctx = nullptr;
+    bool qctx_stale = true;
+    std::vector<float> tri_normal;    // per flattened triangle: face normal (rt_scene_export)
+    std::vector<int32_t> tri_mesh;    // per flattened triangle: mesh index
 
-Renderer::Renderer() : Renderer(Settings{}, true) {}
+    void check(rt_status s, const char* what) const
+    {
+        if (s != RT_OK)
+            throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + (group ? rt_group_last_error(group) : rt_last_error(ctx)));
+    }
+    rt_ctx* query_ctx()
+    {
+        if (ctx) return ctx;
+        if (!qctx) {
+            rt_device_cfg cfg{settings.devices.empty() ? settings.device : settings.devices[0], nullptr, 0};
+            check(rt_create(&qctx, &cfg), "rt_create");
+            qctx_stale = true;
+        }
+        if (qctx_stale) {
+            const rt_status st = rt_upload_scene(qctx, scene);
+            if (st != RT_OK) throw rt::Error(std::string("rt_upload_scene failed: ") + rt_last_error(qctx));
+            qctx_stale = false;
+        }
+        return qctx;
+    }
+    ~Impl()
+    {
+        rt_group_destroy(group);
+        rt_destroy(ctx);
+        rt_destroy(qctx);
+        rt_scene_destroy(scene);
+    }
+};
 
-Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
+Renderer::Renderer(const AbiTag& caller, const Settings& s, bool cornell_box)
+    : abi_(caller, sizeof(Renderer), sizeof(Settings)), impl_(std::make_unique<Impl>())
 {
-    if (rt_api_version() != RT_API_VERSION)   // this header's structs against the loaded library's
-        throw rt::Error("librt_hip.so C-ABI version " + std::to_string(rt_api_version()) + ", include/rt_capi.h " + std::to_string(RT_API_VERSION));
-    if (settings.devices.size() > 1) {
-        check(rt_group_create(&group, settings.devices.data(), (uint32_t)settings.devices.size()), "rt_group_create");
+    Impl& I = *impl_;
+    I.settings = s;
+    if (I.settings.devices.size() > 1) {
+        I.check(rt_group_create(&I.group, I.settings.devices.data(), (uint32_t)I.settings.devices.size()), "rt_group_create");
     } else {
-        rt_device_cfg cfg{settings.devices.empty() ? settings.device : settings.devices[0], nullptr, 0};
-        check(rt_create(&ctx, &cfg), "rt_create");
+        rt_device_cfg cfg{I.settings.devices.empty() ? I.settings.device : I.settings.devices[0], nullptr, 0};
+        I.check(rt_create(&I.ctx, &cfg), "rt_create");
     }
     if (cornell_box) {
         // Renderer::Renderer(): materials + six meshes + GenerateBVH (MC/Renderer.cpp:26-57)
@@ -185,91 +258,78 @@ Renderer::Renderer(const Settings& s, bool cornell_box) : settings(s)
             rt::Material mat;
             mat.diffuse_coefficient = rt::vec3{m.material.albedo.x, m.material.albedo.y, m.material.albedo.z};
             mat.emission = rt::vec3{m.material.emission.x, m.material.emission.y, m.material.emission.z};
-            owned.push_back(std::make_unique<rt::TriangleMesh>(std::move(m.raw), mat));
-            Add(owned.back().get());
+            I.owned.push_back(std::make_unique<rt::TriangleMesh>(std::move(m.raw), mat));
+            Add(I.owned.back().get());
         }
         GenerateBVH();
     }
 }
 
-Renderer::~Renderer()
-{
-    rt_group_destroy(group);
-    rt_destroy(ctx);
-    rt_destroy(qctx);
-    rt_scene_destroy(scene_);
-}
+Renderer::~Renderer() = default;
+
+std::shared_ptr<rt::Image> Renderer::GetFinalImage() const { return impl_->frame_image_final; }
+void Renderer::Reaccumulate() { impl_->frame_accumulating = 1; ++impl_->epoch; }
+uint32_t Renderer::GetSPP() { return impl_->frame_accumulating - 1; }
+Renderer::Settings& Renderer::GetSettings() { return impl_->settings; }
+const rt_scene* Renderer::Scene() const { return impl_->scene; }
 
 void Renderer::GenerateBVH()
 {
+    Impl& I = *impl_;
     rt_scene* sc = nullptr;
-    check(rt_scene_create(&sc), "rt_scene_create");
+    I.check(rt_scene_create(&sc), "rt_scene_create");
     for (rt::Entity* e : entities) {
         const auto& raw = e->RawPositions();
         const rt::Material& m = e->GetMaterial();
         const float alb[3] = {m.diffuse_coefficient.x, m.diffuse_coefficient.y, m.diffuse_coefficient.z};
         const float em[3] = {m.emission.x, m.emission.y, m.emission.z};
         rt_status st = rt_scene_add_mesh(sc, raw.data(), raw.size() / 9, alb, em, nullptr);
-        if (st != RT_OK) { rt_scene_destroy(sc); check(st, "rt_scene_add_mesh"); }
+        if (st != RT_OK) { rt_scene_destroy(sc); I.check(st, "rt_scene_add_mesh"); }
     }
     rt_status st = rt_scene_build(sc);
-    if (st == RT_OK) st = group ? rt_group_upload_scene(group, sc) : rt_upload_scene(ctx, sc);
-    if (st != RT_OK) { rt_scene_destroy(sc); check(st, "GenerateBVH"); }
-    rt_scene_destroy(scene_);
-    scene_ = sc;   // kept for Scene()
-    bvh_dirty = false;
-    qctx_stale = true;
+    if (st == RT_OK) st = I.group ? rt_group_upload_scene(I.group, sc) : rt_upload_scene(I.ctx, sc);
+    if (st != RT_OK) { rt_scene_destroy(sc); I.check(st, "GenerateBVH"); }
+    rt_scene_destroy(I.scene);
+    I.scene = sc;   // kept for Scene()
+    I.bvh_dirty = false;
+    I.qctx_stale = true;
     // the per-triangle records the queries return (face normal, mesh)
     rt_scene_info info{};
-    check(rt_scene_get_info(sc, &info), "rt_scene_get_info");
+    I.check(rt_scene_get_info(sc, &info), "rt_scene_get_info");
     std::vector<float> nf((size_t)info.n_nodes * 7), tf((size_t)info.n_tris * 13);
     std::vector<int32_t> ni((size_t)info.n_nodes * 5), ti((size_t)info.n_tris * 2);
-    check(rt_scene_export(sc, nf.data(), ni.data(), tf.data(), ti.data()), "rt_scene_export");
-    tri_normal_.resize((size_t)info.n_tris * 3);
-    tri_mesh_.resize(info.n_tris);
+    I.check(rt_scene_export(sc, nf.data(), ni.data(), tf.data(), ti.data()), "rt_scene_export");
+    I.tri_normal.resize((size_t)info.n_tris * 3);
+    I.tri_mesh.resize(info.n_tris);
     for (size_t i = 0; i < info.n_tris; ++i) {
-        for (int k = 0; k < 3; ++k) tri_normal_[3 * i + k] = tf[13 * i + 9 + k];
-        tri_mesh_[i] = ti[2 * i];
+        for (int k = 0; k < 3; ++k) I.tri_normal[3 * i + k] = tf[13 * i + 9 + k];
+        I.tri_mesh[i] = ti[2 * i];
     }
-}
-
-rt_ctx* Renderer::query_ctx() const
-{
-    if (ctx) return ctx;
-    if (!qctx) {
-        rt_device_cfg cfg{settings.devices.empty() ? settings.device : settings.devices[0], nullptr, 0};
-        check(rt_create(&qctx, &cfg), "rt_create");
-        qctx_stale = true;
-    }
-    if (qctx_stale) {
-        const rt_status st = rt_upload_scene(qctx, scene_);
-        if (st != RT_OK) throw rt::Error(std::string("rt_upload_scene failed: ") + rt_last_error(qctx));
-        qctx_stale = false;
-    }
-    return qctx;
 }
 
 Renderer::Hit Renderer::Trace(const vec3& origin, const vec3& direction) const
 {
-    if (bvh_dirty || !scene_) throw rt::Error("ray_BVH_intersection_record before GenerateBVH");
-    rt_ctx* q = query_ctx();
+    Impl& I = *impl_;
+    if (I.bvh_dirty || !I.scene) throw rt::Error("ray_BVH_intersection_record before GenerateBVH");
+    rt_ctx* q = I.query_ctx();
     const float o[3] = {origin.x, origin.y, origin.z}, d[3] = {direction.x, direction.y, direction.z};
     int32_t tri = -1;
     double t = 0.0;
     const rt_status st = rt_trace(q, 1, o, d, &tri, &t);
     if (st != RT_OK) throw rt::Error(std::string("rt_trace failed: ") + rt_last_error(q));
     Hit h;
-    if (tri >= 0 && (size_t)tri < tri_mesh_.size()) {
-        h.hit = true; h.t = t; h.triangle = tri; h.mesh = tri_mesh_[tri];
-        h.normal = vec3{tri_normal_[3 * tri], tri_normal_[3 * tri + 1], tri_normal_[3 * tri + 2]};
+    if (tri >= 0 && (size_t)tri < I.tri_mesh.size()) {
+        h.hit = true; h.t = t; h.triangle = tri; h.mesh = I.tri_mesh[tri];
+        h.normal = vec3{I.tri_normal[3 * tri], I.tri_normal[3 * tri + 1], I.tri_normal[3 * tri + 2]};
     }
     return h;
 }
 
 Renderer::LightSample Renderer::SampleLight(const uint32_t draws[3]) const
 {
-    if (bvh_dirty || !scene_) throw rt::Error("SamplingAreaLight before GenerateBVH");
-    rt_ctx* q = query_ctx();
+    Impl& I = *impl_;
+    if (I.bvh_dirty || !I.scene) throw rt::Error("SamplingAreaLight before GenerateBVH");
+    rt_ctx* q = I.query_ctx();
     float loc[3], n[3], em[3], pdf = 0.0f;
     const rt_status st = rt_sample_light(q, 1, draws, loc, n, em, &pdf);
     if (st != RT_OK) throw rt::Error(std::string("rt_sample_light failed: ") + rt_last_error(q));
@@ -278,61 +338,63 @@ Renderer::LightSample Renderer::SampleLight(const uint32_t draws[3]) const
 
 void Renderer::ResizeViewport(uint32_t width, uint32_t height)
 {   // MC/Renderer.cpp:59-89
-    if (frame_image_final) {
-        if (frame_image_final->GetWidth() == width && frame_image_final->GetHeight() == height) return;
-        frame_image_final->Resize(width, height);
+    Impl& I = *impl_;
+    if (I.frame_image_final) {
+        if (I.frame_image_final->GetWidth() == width && I.frame_image_final->GetHeight() == height) return;
+        I.frame_image_final->Resize(width, height);
     } else {
-        frame_image_final = std::make_shared<rt::Image>(width, height);
+        I.frame_image_final = std::make_shared<rt::Image>(width, height);
     }
-    if (group) check(rt_group_resize(group, width, height, settings.band), "rt_group_resize");
-    else check(rt_resize(ctx, width, height, 8, 0, 1), "rt_resize");
-    frame_accumulating = 1;
+    if (I.group) I.check(rt_group_resize(I.group, width, height, I.settings.band), "rt_group_resize");
+    else I.check(rt_resize(I.ctx, width, height, 8, 0, 1), "rt_resize");
+    I.frame_accumulating = 1;
 }
 
 void Renderer::Render(const Camera& camera) { RenderFrames(camera, 1); }
 
 void Renderer::RenderFrames(const Camera& camera, uint32_t n)
 {   // MC/Renderer.cpp:91-122, n frames per launch
-    if (!frame_image_final) throw rt::Error("Render before ResizeViewport");
-    if (bvh_dirty) GenerateBVH();
+    Impl& I = *impl_;
+    if (!I.frame_image_final) throw rt::Error("Render before ResizeViewport");
+    if (I.bvh_dirty) GenerateBVH();
     const rt_camera cam = camera.Native();
-    if (!settings.accumulating) {
+    if (!I.settings.accumulating) {
         // every frame restarts the average (frame_accumulating stays 1, MC/Renderer.cpp:95-98,114-121),
         // so only the last of n frames is visible: render that one, on a fresh RNG epoch so
         // successive frames carry fresh noise like the reference's free-running mt19937
         if (n == 0) return;
-        ++epoch;
+        ++I.epoch;
         n = 1;
     }
-    rt_render_params p{frame_accumulating, n, settings.seed + epoch, RR_survival_probability, settings.exact ? RT_RENDER_EXACT : 0u};
-    if (group) check(rt_group_render(group, &cam, &p, frame_image_final->Data()), "rt_group_render");
-    else check(rt_render(ctx, &cam, &p, frame_image_final->Data(), nullptr), "rt_render");
-    if (settings.accumulating) frame_accumulating += n;
-    else frame_accumulating = 1;
+    rt_render_params p{I.frame_accumulating, n, I.settings.seed + I.epoch, RR_survival_probability, I.settings.exact ? RT_RENDER_EXACT : 0u};
+    if (I.group) I.check(rt_group_render(I.group, &cam, &p, I.frame_image_final->Data()), "rt_group_render");
+    else I.check(rt_render(I.ctx, &cam, &p, I.frame_image_final->Data(), nullptr), "rt_render");
+    if (I.settings.accumulating) I.frame_accumulating += n;
+    else I.frame_accumulating = 1;
 }
 
 const std::vector<float>& Renderer::GetAccumulation()
 {
-    if (group) {
-        accum_host.resize(frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0);
-        if (!accum_host.empty()) check(rt_group_read_accumulation(group, accum_host.data()), "rt_group_read_accumulation");
-        return accum_host;
+    Impl& I = *impl_;
+    const size_t n = I.frame_image_final ? (size_t)I.frame_image_final->GetWidth() * I.frame_image_final->GetHeight() * 4 : 0;
+    I.accum_host.resize(n);
+    if (n) {
+        if (I.group) I.check(rt_group_read_accumulation(I.group, I.accum_host.data()), "rt_group_read_accumulation");
+        else I.check(rt_read_accumulation(I.ctx, I.accum_host.data()), "rt_read_accumulation");
     }
-    const size_t n = frame_image_final ? (size_t)frame_image_final->GetWidth() * frame_image_final->GetHeight() * 4 : 0;
-    accum_host.resize(n);
-    if (n) check(rt_read_accumulation(ctx, accum_host.data()), "rt_read_accumulation");
-    return accum_host;
+    return I.accum_host;
 }
 
 float Renderer::LastKernelMilliseconds() const
 {
-    if (group) {   // the slowest member's band render
+    const Impl& I = *impl_;
+    if (I.group) {   // the slowest member's band render
         rt_group_stats gs{};
-        if (rt_group_get_stats(group, &gs) != RT_OK) return -1.0f;
+        if (rt_group_get_stats(I.group, &gs) != RT_OK) return -1.0f;
         return gs.max_member_kernel_ms;
     }
     rt_stats st{};
-    if (rt_get_stats(ctx, &st) != RT_OK) return -1.0f;
+    if (rt_get_stats(I.ctx, &st) != RT_OK) return -1.0f;
     return st.last_kernel_ms;
 }
 
@@ -349,7 +411,8 @@ void WhittedRenderer::check(rt_status s, const char* what) const
     if (s != RT_OK) throw Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
 }
 
-WhittedRenderer::WhittedRenderer(rt_scene* built_scene, const Settings& s) : settings(s)
+WhittedRenderer::WhittedRenderer(const AbiTag& caller, rt_scene* built_scene, const Settings& s)
+    : abi_(caller, sizeof(WhittedRenderer), sizeof(Settings)), settings(s)
 {
     rt_device_cfg cfg{settings.device, nullptr, 0};
     check(rt_create(&ctx, &cfg), "rt_create");
@@ -420,9 +483,8 @@ void DenoisingRenderer::check(rt_status s, const char* what) const
     if (s != RT_OK) throw Error(std::string(what) + " failed (" + std::to_string(s) + "): " + rt_last_error(ctx));
 }
 
-DenoisingRenderer::DenoisingRenderer() : DenoisingRenderer(Settings{}) {}
-
-DenoisingRenderer::DenoisingRenderer(const Settings& s) : settings(s)
+DenoisingRenderer::DenoisingRenderer(const AbiTag& caller, const Settings& s)
+    : abi_(caller, sizeof(DenoisingRenderer), sizeof(Settings)), settings(s)
 {
     rt_denoise_params_default(&params);   // Denoising::Denoiser's member defaults (DN/Denoiser.h:333-358)
     rt_device_cfg cfg{settings.device, nullptr, 0};

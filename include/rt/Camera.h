@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../rt_capi.h"
+#include "Abi.h"
 
 namespace rt {
 
@@ -33,12 +34,23 @@ struct CameraInput {   // what Walnut::Input provided (MC/Camera.cpp:32-80)
 };
 
 class Camera {
+    // first member: checked against the library's layout before any other member is written (rt/Abi.h)
+    AbiGuard abi_;
+
 public:
-    Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance);
+    Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance)
+        : Camera(AbiTag{RT_CXX_ABI_VERSION, AbiClass::Camera, sizeof(Camera), 0}, verticalFOV, NearClipPlaneDistance,
+                 FarClipPlaneDistance)
+    {
+    }
     // the other projects' cameras differ only in their member defaults: the BVH Ray Tracer at
     // (-1, 5, 10) and the Whitted Style Ray Tracer at (0, 0, 6), both looking down -z
     // (BV/Camera.h:19-20, WH/Camera.h:17-19)
-    Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 position, rt::vec3 forward);
+    Camera(float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 position, rt::vec3 forward)
+        : Camera(AbiTag{RT_CXX_ABI_VERSION, AbiClass::Camera, sizeof(Camera), 0}, verticalFOV, NearClipPlaneDistance,
+                 FarClipPlaneDistance, position, forward)
+    {
+    }
     // what a UpdateCamera key press does to the position (e.g. a scripted camera path); recomputes the view
     void SetPosition(rt::vec3 p);
 
@@ -62,6 +74,10 @@ public:
     rt_camera Native() const;
 
 private:
+    // librt_hip.so
+    Camera(const AbiTag& caller, float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance);
+    Camera(const AbiTag& caller, float verticalFOV, float NearClipPlaneDistance, float FarClipPlaneDistance, rt::vec3 position,
+           rt::vec3 forward);
     void RecomputeProjectionMatrix();
     void RecomputeViewMatrix();
 

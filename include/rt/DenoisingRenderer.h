@@ -19,6 +19,9 @@
 namespace rt {
 
 class DenoisingRenderer {
+    // first member: checked against the library's layout before any other member is written (rt/Abi.h)
+    AbiGuard abi_;
+
 public:
     struct Settings {   // DN/Renderer.h:35-60
         bool immediate_clamping = true;
@@ -41,8 +44,11 @@ public:
         int device = 0;
     };
 
-    DenoisingRenderer();                              // the Cornell box (DN/Renderer.cpp:26-58), device 0
-    explicit DenoisingRenderer(const Settings& s);
+    DenoisingRenderer() : DenoisingRenderer(Settings{}) {}   // the Cornell box (DN/Renderer.cpp:26-58), device 0
+    explicit DenoisingRenderer(const Settings& s)
+        : DenoisingRenderer(AbiTag{RT_CXX_ABI_VERSION, AbiClass::DenoisingRenderer, sizeof(DenoisingRenderer), sizeof(Settings)}, s)
+    {
+    }
     ~DenoisingRenderer();
     DenoisingRenderer(const DenoisingRenderer&) = delete;
     DenoisingRenderer& operator=(const DenoisingRenderer&) = delete;
@@ -60,6 +66,7 @@ public:
     const float RR_survival_probability = 0.8f;              // DN/Renderer.h:226
 
 private:
+    DenoisingRenderer(const AbiTag& caller, const Settings& s);   // librt_hip.so
     void check(rt_status s, const char* what) const;
     void resolve_settings();
     Settings settings;

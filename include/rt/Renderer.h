@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../rt_capi.h"
+#include "Abi.h"
 #include "Camera.h"
 
 namespace rt {
@@ -56,12 +57,10 @@ private:
     std::vector<uint32_t> data_;
 };
 
-class Error : public std::runtime_error {
-public:
-    using std::runtime_error::runtime_error;
-};
-
 class Renderer {
+    // first member: checked against the library's layout before any other member is written (rt/Abi.h)
+    AbiGuard abi_;
+
 public:
     struct Settings {
         bool accumulating = true;
@@ -74,8 +73,11 @@ public:
         uint32_t band = 8;          // rows per band of the multi-GPU split
     };
 
-    Renderer();                                  // Cornell box, device 0
-    explicit Renderer(const Settings& s, bool cornell_box = true);
+    Renderer() : Renderer(Settings{}, true) {}   // Cornell box, device 0
+    explicit Renderer(const Settings& s, bool cornell_box = true)
+        : Renderer(AbiTag{RT_CXX_ABI_VERSION, AbiClass::Renderer, sizeof(Renderer), sizeof(Settings)}, s, cornell_box)
+    {
+    }
     ~Renderer();
     Renderer(const Renderer&) = delete;
     Renderer& operator=(const Renderer&) = delete;
@@ -83,25 +85,26 @@ public:
     void ResizeViewport(uint32_t width, uint32_t height);
     void Render(const Camera& camera);                      // +1 spp
     void RenderFrames(const Camera& camera, uint32_t n);    // +n spp in one launch
-    std::shared_ptr<rt::Image> GetFinalImage() const { return frame_image_final; }
+    std::shared_ptr<rt::Image> GetFinalImage() const;
     const std::vector<float>& GetAccumulation();            // float4 per pixel (host copy)
-    void Reaccumulate() { frame_accumulating = 1; ++epoch; }
-    uint32_t GetSPP() { return frame_accumulating - 1; }
-    Settings& GetSettings() { return settings; }
+    void Reaccumulate();
+    uint32_t GetSPP();
+    Settings& GetSettings();
     [[nodiscard]] const std::vector<rt::Entity*>& GetEntities() const { return entities; }
     void Add(rt::Entity* entity_pointer) { entities.push_back(entity_pointer); }
     void GenerateBVH();
     float LastKernelMilliseconds() const;
     // the flattened scene of the last GenerateBVH (host side: rt_scene_get_info / rt_scene_export), e.g. to
     // check a scene built through Add against the reference's BVH
-    const rt_scene* Scene() const { return scene_; }
+    const rt_scene* Scene() const;
 
     // The reference Renderer's scene queries on the scene of the last GenerateBVH, answered by this library's
     // device kernels (rt_trace / rt_sample_light: the path kernels' own traversal and light sampling).  One ray
     // or one sample per call, a kernel launch and a synchronisation each; batch through the C-ABI for many.
     // ray_BVH_intersection_record (MC/Renderer.h:88-91 -> BVH::traverse_BVH_from_root, MC/BVH.h:72-101):
-    // the closest hit's double t, its triangle (flattened slot), the mesh it belongs to (index into
-    // GetEntities()) and the triangle's face normal (MC/TriangleMesh.h:57-59,118-134)
+    // the closest hit's double t, its triangle (flattened slot), the entity it belongs to (index into
+    // GetEntities()) and the surface normal at the hit (a triangle's face normal, MC/TriangleMesh.h:57-59,118-134;
+    // a sphere's normalize(location - center), MC/Sphere.h:89-94)
     struct Hit { bool hit = false; double t = 1.7976931348623157e308; int32_t triangle = -1; int32_t mesh = -1; vec3 normal{}; };
     Hit Trace(const vec3& origin, const vec3& direction) const;
     // SamplingAreaLight (MC/Renderer.h:163-180) on three given Walnut::Random words (area pick, triangle x,
@@ -110,26 +113,14 @@ public:
     LightSample SampleLight(const uint32_t draws[3]) const;
 
     float RR_survival_probability = 0.8f;        // MC/Renderer.h:199
-    std::vector<rt::Entity*> entities;
+    std::vector<rt::Entity*> entities;           // MC/Renderer.h:201
 
 private:
-    void check(rt_status s, const char* what) const;
-    Settings settings;
-    std::shared_ptr<rt::Image> frame_image_final;
-    std::vector<float> accum_host;
-    uint32_t frame_accumulating = 1;
-    uint64_t epoch = 0;
-    rt_ctx* ctx = nullptr;
-    rt_group* group = nullptr;   // Settings::devices with more than one entry
-    std::vector<std::unique_ptr<rt::Entity>> owned;   // the built-in Cornell meshes
-    rt_scene* scene_ = nullptr;
-    bool bvh_dirty = true;
-    // the queries' context: ctx, or (several devices) one on the first device holding the scene
-    rt_ctx* query_ctx() const;
-    mutable rt_ctx* qctx = nullptr;
-    mutable bool qctx_stale = true;
-    std::vector<float> tri_normal_;    // per flattened triangle: face normal (rt_scene_export)
-    std::vector<int32_t> tri_mesh_;    // per flattened triangle: mesh index
+    Renderer(const AbiTag& caller, const Settings& s, bool cornell_box);   // librt_hip.so
+    // everything else lives behind one pointer, so that the library's state can grow without changing the
+    // layout a caller allocates
+    struct Impl;
+    std::unique_ptr<Impl> impl_;
 };
 
 }  // namespace rt

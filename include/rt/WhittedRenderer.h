@@ -28,6 +28,9 @@ struct WhittedSettings {
 };
 
 class WhittedRenderer {
+    // first member: checked against the library's layout before any other member is written (rt/Abi.h)
+    AbiGuard abi_;
+
 public:
     using Settings = WhittedSettings;
     // the two reference worlds
@@ -39,7 +42,10 @@ public:
     static Camera BVHRayTracerCamera() { return Camera(35.0f, 0.1f, 100.0f, vec3{-1.0f, 5.0f, 10.0f}, vec3{0.0f, 0.0f, -1.0f}); }
 
     // any world built through the C-ABI scene builder (rt_scene_add_world_* or rt_scene_add_whitted_*)
-    WhittedRenderer(rt_scene* built_scene, const Settings& s);
+    WhittedRenderer(rt_scene* built_scene, const Settings& s)
+        : WhittedRenderer(AbiTag{RT_CXX_ABI_VERSION, AbiClass::WhittedRenderer, sizeof(WhittedRenderer), sizeof(Settings)}, built_scene, s)
+    {
+    }
     ~WhittedRenderer();
     WhittedRenderer(const WhittedRenderer&) = delete;
     WhittedRenderer& operator=(const WhittedRenderer&) = delete;
@@ -54,6 +60,7 @@ public:
     float LastKernelMilliseconds() const;
 
 private:
+    WhittedRenderer(const AbiTag& caller, rt_scene* built_scene, const Settings& s);   // librt_hip.so
     void check(rt_status s, const char* what) const;
     Settings settings;
     std::shared_ptr<Image> frame_image_final;

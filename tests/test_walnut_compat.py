@@ -48,6 +48,7 @@ def render(cam, frames, seed, rr):
 def test_reference_layer_runs_on_the_dropin(tmp_path):
     if not os.path.exists(WB.BIN):
         pytest.skip("tests/_bin/walnut_mainloop not built (build() builds it where /root/reference exists)")
+    assert not WB.headers_changed(WB.BIN), "tests/_bin/walnut_mainloop predates the drop-in headers: rerun build()"
     prefix = str(tmp_path / "frame")
     r = subprocess.run([WB.BIN, prefix], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -89,6 +90,7 @@ def test_scene_extension_builds_c5(tmp_path):
     import _oracle as O
     if not os.path.exists(WB.C5_BIN):
         pytest.skip("tests/_bin/walnut_c5_scene not built (build() builds it)")
+    assert not WB.headers_changed(WB.C5_BIN), "tests/_bin/walnut_c5_scene predates the drop-in headers: rerun build()"
     fx = np.load(os.path.join(O.GOLDEN, "c5_scene.npz"))
     bunny = np.load(os.path.join(O.GOLDEN, "bvh_scene.npz"))["raw_bunny"]
     obj = str(tmp_path / "c5_bunny.obj")

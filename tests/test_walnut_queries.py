@@ -44,6 +44,7 @@ def test_optics_fixture_shape():
 def test_renderer_queries_match_reference(tmp_path):
     if not os.path.exists(WB.QUERIES_BIN):
         pytest.skip("tests/_bin/walnut_queries not built (build() builds it)")
+    assert not WB.headers_changed(WB.QUERIES_BIN), "tests/_bin/walnut_queries predates the drop-in headers: rerun build()"
     rays = np.load(os.path.join(G, "rays_cornell.npz"))
     light = np.load(os.path.join(G, "light_cases.npz"))
     optics = np.load(os.path.join(G, "optics_cases.npz"))
