@@ -282,6 +282,108 @@ def frame_parity(ctx, gat, W, H, spp, args, world, dist, torch, dev, gloo, use_d
     return out
 
 
+# C5 (BASELINE.json configs[4]): the Cornell box + the 79,488-triangle mesh (the bunny subdivided 1:4 twice,
+# rt.c5_mesh), 3840x2160 at 4096 spp, secondary to the headline: the reference's work per sample (oracle
+# counters at C5, tools/bench_configs.py WORK) priced as for C4
+C5_WORK = (3.660, 31.30, 3.85)   # rays per sample, node tests per ray, triangle tests per ray
+C5_FLOPS_PER_SAMPLE = C5_WORK[0] * (C5_WORK[1] * 18 + C5_WORK[2] * 54) + 0.4036 * C5_WORK[0] * 150
+
+
+def c5_counters(kname, W, H, spp, passes, digest):
+    """The PMC summary of a rocprofv3 pass of this build on C5's frame: the exact shape if one is committed,
+    else the same frame at another spp (the counters are per sample; frames are i.i.d.)."""
+    import glob
+    exact, other = f"{kname}:{W}x{H}x{spp}_exact_n1_p{passes}", f"{kname}:{W}x{H}x"
+    best = None
+    for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "**", "pmc_summary*.json"), recursive=True), reverse=True):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        k = d.get("key") or ""
+        if digest is None or d.get("lib_sha256") != digest or not k.startswith(other) or "_exact_n1_" not in k:
+            continue
+        d["_file"] = os.path.relpath(p, REPO)
+        if k == exact:
+            return d
+        best = best or d
+    return best
+
+
+def c5_config(rt, dev_index, stream, spp, fast):
+    """C5 after the headline's timed region: one full-spp warm-up render (it allocates the
+    parked-sample and camera-record buffers of all passes), then ONE timed render of 3840x2160 x spp from frame
+    1 (seed 0, RR 0.8), synchronised on both sides; the roofline of its path kernel as bench.py prices C4's;
+    parity of that render against the reference harness's frame (tests/golden/full_c5_4096.npz: every 64th row
+    at 4096 spp, bitwise, and the SHA-256 of those rows; full_c5.npz: the whole 256-spp frame)."""
+    import hashlib
+
+    import torch
+    bvh = np.load(os.path.join(REPO, "tests", "golden", "bvh_scene.npz"))
+    W, H = 3840, 2160
+    t_up = time.perf_counter()
+    ctx = rt.Context(dev_index, stream.cuda_stream)
+    try:
+        ctx.upload(rt.Scene.cornell_c5(bvh["raw_bunny"]))
+        ctx.resize(W, H)
+        scene_s = time.perf_counter() - t_up
+        cam, _, _ = rt.camera_default(W, H)
+        ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not fast, fetch=False)   # warm-up, full spp
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not fast, fetch=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        st = ctx.stats()
+        samples = W * H * spp
+        passes = max(1, int(st.n_passes))
+        main_s, pre_s = st.last_main_ms / 1e3, st.last_prepass_ms / 1e3
+        kname = rt.KERNEL_NAMES.get(st.kernel, str(st.kernel))
+        digest = lib_digest(os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so"))
+        achieved = C5_FLOPS_PER_SAMPLE * samples / (main_s + pre_s) / 1e12
+        roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / VALU_PEAK_TFLOPS, 4), "kernel": kname + " + camera_prepass_kernel",
+                "kernel_ms": round((main_s + pre_s) * 1e3, 3), "path_kernel_ms": round(main_s * 1e3, 3),
+                "prepass_ms": round(pre_s * 1e3, 3), "dominant_frac": round(C5_FLOPS_PER_SAMPLE * samples / main_s / 1e12 / VALU_PEAK_TFLOPS, 4),
+                "flops_per_sample": round(C5_FLOPS_PER_SAMPLE, 1), "lib_sha256": digest, "counters": None, "traffic": None}
+        pmc = c5_counters(kname, W, H, spp, passes, digest)
+        if pmc is not None:
+            roof["counters"] = {"file": pmc["_file"], "profiled_key": pmc.get("key"),
+                                "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"), "valu_issue_frac": pmc.get("valu_issue_frac"),
+                                "valu_lane_utilization": pmc.get("valu_lane_utilization"), "wait_any_frac": pmc.get("wait_any_frac"),
+                                "l2_hit_rate": pmc.get("l2_hit_rate"), "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample")}
+            if pmc.get("hbm_bytes_per_sample") is not None:
+                roof["traffic"] = round(pmc["hbm_bytes_per_sample"] * samples / passes, 1)   # bytes per launch (pass)
+                roof["fabric_frac_of_hbm_peak"] = round(pmc["hbm_bytes_per_sample"] * samples / main_s / HBM_PEAK_BYTES_PER_S, 4)
+        parity = None
+        for name in ("full_c5_4096", "full_c5"):
+            p = os.path.join(REPO, "tests", "golden", f"{name}.npz")
+            if fast or not os.path.exists(p):
+                continue
+            z = np.load(p)
+            if (int(z["W"]), int(z["H"]), int(z["spp"])) != (W, H, spp):
+                continue
+            acc = ctx.accumulation()
+            rows = z["rows"]
+            a, b = acc[rows, :, :3], z["accum_rows"]
+            same = np.all(a.view(np.uint32) == b.view(np.uint32), axis=-1)
+            ca = np.clip(a / np.float32(spp), 0.0, 1.0).astype(np.float64)
+            cb = np.clip(b / np.float32(spp), 0.0, 1.0).astype(np.float64)
+            sel = np.ascontiguousarray(acc[rows] if bool(z["rows_only"]) else acc)
+            sha = hashlib.sha256(sel.tobytes()).hexdigest() == str(z["sha_accum"])
+            parity = {"fixture": f"tests/golden/{name}.npz", "rows_checked": int(len(rows)),
+                      "scope": "every 64th row" if bool(z["rows_only"]) else "whole frame",
+                      "rmse_vs_ref": float(np.sqrt(np.mean((ca - cb) ** 2))), "bitwise_frac": round(float(same.mean()), 6),
+                      "sha_accum_match": sha, "sha_match": bool(sha and same.all())}
+            break
+        return {"workload": f"C5 cornell+c5_mesh {W}x{H} {spp}spp", "triangles": 79520, "msamples_per_s": round(samples / dt / 1e6, 2),
+                "render_s": round(dt, 4), "render_ms_with_finalize": round(st.last_kernel_ms, 3), "passes": passes,
+                "kernel": kname, "scene_build_and_upload_s": round(scene_s, 3), "roofline": roof, "parity": parity,
+                "timing": "one timed render after one full-spp warm-up, torch.cuda.synchronize() on both sides"}
+    finally:
+        ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -302,6 +404,8 @@ def main():
                     help="run the N > 1 path's collectives even with one rank: init_process_group, the all-gather of "
                          "the bands and the MAX all-reduce of the time (exercises RCCL on a one-GPU box)")
     ap.add_argument("--dump-image", default=None, help="rank 0 saves the gathered RGBA8 frame (.npy, row 0 = bottom)")
+    ap.add_argument("--no-c5", action="store_true", help="skip the secondary C5 line (configs.c5; N = 1 only)")
+    ap.add_argument("--c5-spp", type=int, default=4096)
     args = ap.parse_args()
 
     import torch
@@ -344,16 +448,22 @@ def main():
     stage = torch.zeros(gat.max_rows * W, dtype=torch.int32, device=dev) if gloo else None
     assert gat.n_local == ctx.local_rows
     kernel_ms, main_ms, pre_ms = [], [], []
+    marks = []   # per step: events on the shared stream before the render, after it, after the gather
     launch_info = {}
 
     def step():
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
         ctx.render(cam, spp, first_frame=1, seed=0, rr=0.8, exact=not args.fast, fetch=False)
+        e[1].record(stream)
         if gloo:   # host-staged bands: the device rows, then the gloo all-gather of host tensors
             ctx.copy_rgba_to_device(stage.data_ptr())
             gat.send.copy_(stage.cpu())
         else:
             ctx.copy_rgba_to_device(gat.send.data_ptr())   # this rank's rows, on the shared stream
         gat.gather()                                        # all-gather + reassembly on rank 0
+        e[2].record(stream)
+        marks.append(e)
         st = ctx.stats()
         kernel_ms.append(st.last_kernel_ms)
         main_ms.append(st.last_main_ms)
@@ -362,7 +472,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    kernel_ms.clear(); main_ms.clear(); pre_ms.clear()
+    kernel_ms.clear(); main_ms.clear(); pre_ms.clear(); marks.clear()
     torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
@@ -370,10 +480,18 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    t_done = time.perf_counter()
     if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # where this rank's time went: the render (pre-pass + path kernel + finalize, the
+    # library's HIP events), the band copy + gather (events on the shared stream; for gloo the host-staged
+    # copy and the host all-gather), and the wait in the closing barrier for the slowest rank
+    rank_parts = np.array([sum(kernel_ms), sum(main_ms), sum(pre_ms),
+                           sum(m[1].elapsed_time(m[2]) for m in marks), (time.perf_counter() - t_done) * 1e3,
+                           sum(m[0].elapsed_time(m[1]) for m in marks), elapsed * 1e3], np.float64)
     per_rank = [elapsed]
+    all_parts = [rank_parts]
     if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
         parts = [torch.zeros_like(t) for _ in range(world)]
@@ -381,6 +499,12 @@ def main():
         per_rank = [float(x.item()) for x in parts]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        tp = torch.tensor(rank_parts, dtype=torch.float64, device=torch.device("cpu") if gloo else dev)
+        gp = [torch.zeros_like(tp) for _ in range(world)]
+        dist.all_gather(gp, tp)
+        all_parts = [x.cpu().numpy() for x in gp]
+    rank_times = {k: [round(float(p[i]), 3) for p in all_parts] for i, k in enumerate(
+        ("render_ms", "kernel_ms", "prepass_ms", "gather_ms", "barrier_wait_ms", "render_events_ms", "elapsed_ms"))}
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
     if args.dump_image and rank == 0:
@@ -449,6 +573,13 @@ def main():
                 "exact_msamples_per_s_kernels_rank": round(local_samples / (k_s * passes) / 1e6, 1),
                 "exact_cost": round(k_s * passes / fk - 1.0, 4)}
 
+    # the headline context's buffers (tens of GB of parked samples and camera records) go before C5's
+    ctx.close()
+    ctx = None
+    configs = None
+    if world == 1 and not args.no_c5:
+        configs = {"c5": c5_config(rt, dev.index, stream, args.c5_spp, args.fast)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(W, H, args.cpu_seconds)
@@ -471,12 +602,17 @@ def main():
             "parity": parity,
             "fast_mode": fast,
             "rank_elapsed_s": [round(x, 6) for x in per_rank],
+            # per rank, summed over the timed steps (ms): render = pre-pass + path kernel + finalize (the library's
+            # events; kernel = the path kernel, prepass = the camera pre-pass, both inside render), gather = band
+            # copy + all-gather, barrier_wait = the closing barrier; render + gather + barrier_wait <= elapsed
+            "rank_times_ms": rank_times,
             "collectives": ({"backend": args.dist_backend, "ops": ["all_gather_into_tensor" if not gloo else "all_gather", "all_gather", "all_reduce(MAX)", "barrier"],
                              "forced_one_rank": world == 1} if use_dist else None),
             "cpu_baseline": cpu,
+            # secondary configurations, measured after the headline's timed region (value stays C4)
+            "configs": configs,
         }
         print(json.dumps(line), flush=True)
-    ctx.close()
     if use_dist:
         dist.destroy_process_group()
 

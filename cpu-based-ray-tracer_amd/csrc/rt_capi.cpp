@@ -114,6 +114,7 @@ struct rt_ctx {
     size_t tile_words = 0;
     int lds_levels_force = -1;   // diagnostic: fold-stack levels in LDS (RT_LDS_LEVELS), occupancy permitting or not
     bool brute = true;   // small scenes: coherent trace over the distinct leaf boxes (RT_BRUTE=0 disables)
+    bool direct_div2 = true;   // the direct term's two divisions on Markstein's path when in range (RT_DIRECT_DIV2=0: IEEE, A/B)
     bool sky_bits = true;   // the pre-pass's camera-ray misses as bits, not parked samples (RT_SKY_BITS=0 disables)
     bool force_walk = false;   // diagnostic: the vertex kernel's per-lane BVH walk for every ray (RT_FORCE_WALK=1)
     bool vertex = true;  // small scenes: the vertex-synchronous kernel, rt_coherent.hip (RT_VERTEX=0: the megakernel's coherent trace)
@@ -460,6 +461,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_LDS_LEVELS")) c->lds_levels_force = (int)std::strtol(e, nullptr, 10);
     if (const char* e = rt_knob("RT_BRUTE")) c->brute = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SKY_BITS")) c->sky_bits = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_DIRECT_DIV2")) c->direct_div2 = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_VERTEX")) c->vertex = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
@@ -772,10 +774,12 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         P.y_pdf = 1.0f / pdf;
         P.y_rr = p->rr > 0.0f ? 1.0f / p->rr : 0.0f;
         P.rr_fast = (p->rr >= 0x1p-20f && p->rr < 1.0f) ? 1u : 0u;
-        P.lpdf_fast = (P.lpdf >= 0x1p-20f && P.lpdf < 0x1p20f) ? 1u : 0u;
         P.wh_fast = (c->W >= 1u && c->W < (1u << 20) && c->H >= 1u && c->H < (1u << 20)) ? 1u : 0u;
         P.lpdf = 1.0f / c->hdr.light_area;
         P.y_lpdf = 1.0f / P.lpdf;
+        // the direct term's (X / dist^2) / lpdf on Markstein's path (rt_coherent.hip): the light PDF must lie in
+        // div_fast's verified divisor range [2^-20, 2^20) (rt_device.h div2_core); RT_DIRECT_DIV2=0 is the A/B
+        P.lpdf_fast = (c->direct_div2 && P.lpdf >= 0x1p-20f && P.lpdf < 0x1p20f) ? 1u : 0u;
         P.y_w = 1.0f / (float)c->W; P.y_h = 1.0f / (float)c->H;
     }
     P.band = c->band; P.rank = c->rank; P.nranks = c->nranks; P.n_local_rows = c->local_rows;
@@ -815,20 +819,22 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // (the BVH variant stages the materials and light tables in LDS with its lane state: a scene whose tables
     // exceed kMaxBvhSmallLds renders on the megakernel)
     const size_t bvh_small_bytes = (size_t)(2 * P.n_mats + P.n_lnodes + 4 * P.n_ltris + 3 * P.n_split_leaves) * sizeof(float4);
-    const bool coh_bvh = !coh_box && c->vertex && c->vertex_bvh && !count && !c->gb_next && !whitted && P.n_tris < (1u << 31) &&
-                         P.n_mats < (1u << 14) && bvh_small_bytes <= kMaxBvhSmallLds;
+    // what keeps a path scene off the BVH variant, RT_KERNEL_REASON_DEFAULT when nothing does: ONE list of
+    // predicates, so that every fallback to the megakernel reports its own reason (rt_stats.kernel_reason;
+    // ADVICE r04/r05)
+    const uint32_t bvh_block = [&]() -> uint32_t {
+        if (count || c->gb_next) return RT_KERNEL_REASON_MODE;
+        if (!c->vertex || !c->vertex_bvh) return RT_KERNEL_REASON_KNOB;
+        if (P.n_tris >= (1u << 31)) return RT_KERNEL_REASON_TRIANGLES;
+        if (P.n_mats >= (1u << 14)) return RT_KERNEL_REASON_MATERIALS;
+        if (bvh_small_bytes > kMaxBvhSmallLds) return RT_KERNEL_REASON_TABLES_LDS;
+        return RT_KERNEL_REASON_DEFAULT;
+    }();
+    const bool coh_bvh = !coh_box && !whitted && bvh_block == RT_KERNEL_REASON_DEFAULT;
     const bool coh = coh_box || coh_bvh;
-    // why this kernel (rt_stats.kernel_reason; ADVICE r04: the BVH variant's LDS-table limit is a cliff the caller
-    // could not see)
     uint32_t reason = RT_KERNEL_REASON_DEFAULT;
-    if (!coh && !whitted) {
-        if (count || c->gb_next) reason = RT_KERNEL_REASON_MODE;
-        else if (!c->vertex || (!c->vertex_bvh && !(P.n_lboxes > 0 && lds))) reason = RT_KERNEL_REASON_KNOB;
-        else if (P.n_mats >= (1u << 14)) reason = RT_KERNEL_REASON_MATERIALS;
-        else if (bvh_small_bytes > kMaxBvhSmallLds) reason = RT_KERNEL_REASON_TABLES_LDS;
-    } else if (coh_bvh && !c->brute && c->hdr.n_lboxes > 0) {
-        reason = RT_KERNEL_REASON_KNOB;   // RT_BRUTE=0: a small scene on the BVH variant
-    }
+    if (!coh && !whitted) reason = bvh_block;
+    else if (coh_bvh && !c->brute && c->hdr.n_lboxes > 0) reason = RT_KERNEL_REASON_KNOB;   // RT_BRUTE=0: a small scene on the BVH variant
     // the camera pre-pass: the leaf-box variant always; the BVH variant for a split scene, whose camera rays are
     // traced like the path kernel's split phase (records carry the triangle in 19 bits, rt_kernels.h crec)
     const bool prepass = coh_box || (coh_bvh && c->bvh_prepass && P.split_root != 0u && P.n_tris < (1u << 19) - 1u);
@@ -984,6 +990,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
                     // in 2^seg_tail_extra times as many parts, no finer than one frame's worth of records
                     Q.seg_tail_shift = std::min(ps + c->seg_tail_extra, lf);
                     Q.seg_tail_n = (uint32_t)std::min<uint64_t>(((uint64_t)c->seg_tail_parts * waves) >> ps, 0xFFFFFFFFull);
+                    if (c->seg_parts_off) { Q.seg_tail_shift = 0; Q.seg_tail_n = 0; }   // the A/B baseline has no finer tail either
                     Q.seg_frames = 1u << lf;
                     Q.seg_shift = 6 + lf;
                     const uint64_t nseg = (uint64_t)Q.n_tiles * ((nf + Q.seg_frames - 1) / Q.seg_frames);

@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             if ((!PRE || BVH) && !pend) {
                 // the camera ray's hit (cast_path, MC/Renderer.cpp:136-146)
                 if (triA < 0) {   // miss: night sky (:145)
-                    L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
+                    L = night_sky();
                     finished = true;
                 } else if (emissive) {   // direct emission (:151-161)
                     const float4 em = S.mats[2 * mat + 1];
@@ -1729,7 +1729,7 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
             surface = true;
             rec = make_float4(d.x, d.y, d.z, __uint_as_float(CREC_CAMERA | (lane << 19) | (j << 25)));
         } else if (valid) {
-            V3 L{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};   // cast_path miss: night sky (MC/Renderer.cpp:145)
+            V3 L = night_sky();   // cast_path miss: night sky (MC/Renderer.cpp:145)
             if (tri >= 0) {
                 const int mat = f2i(S.tris[4 * tri].w);
                 if (S.mats[2 * mat].w != 0.0f) {   // direct emission (MC/Renderer.cpp:151-161)

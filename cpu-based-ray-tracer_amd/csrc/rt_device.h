@@ -13,6 +13,10 @@
 namespace rtd {
 
 struct V3 { float x, y, z; };
+// cast_path's miss radiance, the night sky (12, 20, 69) / 255 (MC/Renderer.cpp:145): one definition for every
+// kernel that adds it (the path kernels, the camera pre-pass, the finalize of the pre-pass's sky bits, the resample)
+constexpr float kNightSkyR = 12 / 255.0f, kNightSkyG = 20 / 255.0f, kNightSkyB = 69 / 255.0f;
+__device__ __forceinline__ V3 night_sky() { return V3{kNightSkyR, kNightSkyG, kNightSkyB}; }
 
 __device__ __forceinline__ V3 mk(float x, float y, float z) { return V3{x, y, z}; }
 __device__ __forceinline__ V3 add(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }

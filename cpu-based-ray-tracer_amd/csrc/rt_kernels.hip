@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 }
                 if (depth == 0) {
                     if (ttri < 0) {   // cast_path miss: night sky (MC/Renderer.cpp:145)
-                        L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};
+                        L = night_sky();
                         finished = true;
                     } else if (emissive) {   // direct emission (MC/Renderer.cpp:151-161)
                         const float4 em = S.mats[2 * mat + 1];
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(256) finalize_chunks_kernel(KParams P, uint32_
     const uint32_t nfp = P.park_all ? P.n_frames : P.n_frames - P.chunk_frames;
     // the pre-pass's sky bits (KParams::sky_bits): a camera-ray miss adds the night sky's radiance, which the pre-pass
     // would have parked (cast_path, MC/Renderer.cpp:145); a 4-frame block of misses is not read at all
-    const float SKY_R = 12 / 255.0f, SKY_G = 20 / 255.0f, SKY_B = 69 / 255.0f;
+    const float SKY_R = kNightSkyR, SKY_G = kNightSkyG, SKY_B = kNightSkyB;
     uint32_t skyw = 0;
     for (uint32_t b = 0; b * 4u < nfp; ++b) {
         if (P.sky_bits != nullptr && (b & 7u) == 0u) skyw = P.sky_bits[(size_t)(b >> 3) * P.lbuf_stride + i];

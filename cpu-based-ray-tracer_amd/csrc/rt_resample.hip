@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) resample_kernel(KParams P)
         V3 L{0.f, 0.f, 0.f};
         int top = -1;   // levels top..0 are folded into L
         if (tri < 0) {
-            L = V3{12 / 255.0f, 20 / 255.0f, 69 / 255.0f};   // cast_path miss, MC/Renderer.cpp:145
+            L = night_sky();   // cast_path miss, MC/Renderer.cpp:145
         } else if (S.mats[2 * f2i(S.tris[4 * tri].w)].w != 0.0f) {
             const float4 em = S.mats[2 * f2i(S.tris[4 * tri].w) + 1];   // direct emission, MC/Renderer.cpp:151-161
             L = V3{em.x, em.y, em.z};

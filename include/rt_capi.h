@@ -254,6 +254,7 @@ typedef struct {
 #define RT_KERNEL_REASON_MATERIALS 2     /* megakernel: 2^14 materials or more (the vertex kernel packs 14 bits) */
 #define RT_KERNEL_REASON_MODE 3          /* megakernel: a work-counter render or a denoiser G-buffer frame */
 #define RT_KERNEL_REASON_KNOB 4          /* a debug knob (RT_VERTEX / RT_VERTEX_BVH / RT_BRUTE) chose it */
+#define RT_KERNEL_REASON_TRIANGLES 5     /* megakernel: 2^31 triangles or more (the BVH variant indexes triangles in 31 bits) */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 /* diagnostic: the raw device counters of the last rt_render (up to 512 x u64; [16..23] = wave cycles per
  * section and [24..43] = wave-level event counts of the vertex kernel in RT_SECTIONS builds, [64..511]

@@ -50,6 +50,18 @@ def test_bench_gloo_matches_one_rank(tmp_path, world, W, H):
     # value is the whole job over the slowest rank's time
     assert abs(line["value"] - W * H * SPP * 2 / max(ranks) / 1e6) <= 1e-2 * line["value"]
     assert line["roofline"]["kernel_ms"] > 0
+    # where each rank's time went: per rank, the render, the band gather and the closing
+    # barrier's wait are disjoint intervals of its timed region
+    rt_ms = line["rank_times_ms"]
+    for k in ("render_ms", "kernel_ms", "prepass_ms", "gather_ms", "barrier_wait_ms", "render_events_ms", "elapsed_ms"):
+        assert len(rt_ms[k]) == world, k
+    for i in range(world):
+        parts = rt_ms["render_events_ms"][i] + rt_ms["gather_ms"][i] + rt_ms["barrier_wait_ms"][i]
+        assert parts <= rt_ms["elapsed_ms"][i] * 1.01 + 1.0, (i, parts, rt_ms["elapsed_ms"][i])
+        assert rt_ms["kernel_ms"][i] + rt_ms["prepass_ms"][i] <= rt_ms["render_ms"][i] * 1.01 + 0.5
+        assert rt_ms["render_ms"][i] <= rt_ms["render_events_ms"][i] * 1.01 + 0.5
+        assert rt_ms["kernel_ms"][i] > 0 and rt_ms["gather_ms"][i] > 0
+        assert abs(rt_ms["elapsed_ms"][i] - 1e3 * ranks[i]) <= 0.01 * rt_ms["elapsed_ms"][i] + 0.5
     gathered = np.load(img)
     c = rt.Context(0)
     try:
@@ -73,7 +85,7 @@ def test_bench_rccl_branch_one_rank(tmp_path, W, H, spp):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "1", "--force-dist", "--dist-backend", "nccl",
            "--steps", "2", "--warmup", "1", "--width", str(W), "--height", str(H), "--spp", str(spp), "--no-cpu-baseline",
-           "--no-fast-probe", "--dump-image", str(img)]
+           "--no-fast-probe", "--no-c5", "--dump-image", str(img)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
