@@ -17,7 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
 
 # include/rt_capi.h RT_API_VERSION: the struct layouts (rt_stats, rt_scene_info, ...) this binding declares
-API_VERSION = 3
+API_VERSION = 4
 
 RT_OK = 0
 RT_ERR_OVERFLOW = -6
@@ -65,6 +65,7 @@ _DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_order
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 # rt_stats.kernel_reason (include/rt_capi.h RT_KERNEL_REASON_*)
 KERNEL_REASON_DEFAULT, KERNEL_REASON_TABLES_LDS, KERNEL_REASON_MATERIALS, KERNEL_REASON_MODE, KERNEL_REASON_KNOB = 0, 1, 2, 3, 4
+KERNEL_REASON_TRIANGLES, KERNEL_REASON_SPHERES = 5, 6
 
 
 class DenoiseParams(C.Structure):
@@ -87,7 +88,8 @@ class SceneInfo(C.Structure):
     _fields_ = [("n_meshes", C.c_uint32), ("n_tris", C.c_uint32), ("n_nodes", C.c_uint32), ("n_light_tris", C.c_uint32),
                 ("max_depth", C.c_uint32), ("light_mesh", C.c_int32), ("light_area", C.c_float), ("device_bytes", C.c_uint64),
                 ("n_leaf_boxes", C.c_uint32), ("n_light_skip", C.c_uint32),
-                ("split_root", C.c_uint32), ("split_end", C.c_uint32), ("n_split_leaves", C.c_uint32), ("n_split_boxes", C.c_uint32)]
+                ("split_root", C.c_uint32), ("split_end", C.c_uint32), ("n_split_leaves", C.c_uint32), ("n_split_boxes", C.c_uint32),
+                ("n_spheres", C.c_uint32)]
 
 
 def _fp(a):
@@ -110,6 +112,7 @@ def lib():
         "rt_scene_add_cornell_box": (i32, [vp]),
         "rt_scene_add_obj": (i32, [vp, C.c_char_p, fp, fp, C.POINTER(i32)]),
         "rt_scene_add_mesh": (i32, [vp, fp, u64, fp, fp, C.POINTER(i32)]),
+        "rt_scene_add_sphere": (i32, [vp, fp, C.c_float, fp, fp, C.POINTER(i32)]),
         "rt_scene_add_whitted_mesh": (i32, [vp, fp, u64, C.c_float, fp, fp, C.c_float, C.POINTER(i32)]),
         "rt_scene_add_whitted_obj": (i32, [vp, C.c_char_p, C.c_float, fp, fp, C.c_float, C.POINTER(i32)]),
         "rt_scene_add_point_light": (i32, [vp, fp, fp]),
@@ -214,6 +217,15 @@ class Scene:
         self._check(lib().rt_scene_add_mesh(self.h, _fp(raw), raw.shape[0], _fp(np.asarray(albedo, np.float32)),
                                             _fp(np.asarray(emission, np.float32)), C.byref(mid)), "rt_scene_add_mesh")
         return mid.value
+
+    def add_sphere(self, center, radius, albedo, emission=(0.0, 0.0, 0.0)):
+        """Renderer::Add(new Whitted::Sphere(center, radius, material)) (MC/Sphere.h:16-108): an entity of the
+        path-traced scene; returns its entity index."""
+        eid = C.c_int32()
+        self._check(lib().rt_scene_add_sphere(self.h, _fp(np.asarray(center, np.float32)), float(radius),
+                                              _fp(np.asarray(albedo, np.float32)), _fp(np.asarray(emission, np.float32)),
+                                              C.byref(eid)), "rt_scene_add_sphere")
+        return eid.value
 
     def add_obj(self, path, albedo, emission):
         mid = C.c_int32()

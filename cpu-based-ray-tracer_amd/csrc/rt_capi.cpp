@@ -253,6 +253,17 @@ rt_status rt_scene_add_mesh(rt_scene* s, const float* raw, uint64_t n_tris, cons
     return RT_OK;
 }
 
+rt_status rt_scene_add_sphere(rt_scene* s, const float center[3], float radius, const float albedo[3], const float emission[3],
+                              int32_t* entity_id)
+{
+    if (!s || !center || !albedo || !emission || !(radius > 0.0f) || !std::isfinite(radius)) return RT_ERR_INVALID;
+    const int id = s->builder.add_sphere(rt::F3{center[0], center[1], center[2]}, radius,
+                                         rt::MaterialDesc{{albedo[0], albedo[1], albedo[2]}, {emission[0], emission[1], emission[2]}});
+    if (entity_id) *entity_id = id;
+    s->built = false;
+    return RT_OK;
+}
+
 rt_status rt_scene_add_obj(rt_scene* s, const char* path, const float albedo[3], const float emission[3], int32_t* mesh_id)
 {
     if (!s || !path || !albedo || !emission) return RT_ERR_INVALID;
@@ -416,6 +427,7 @@ rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info)
     info->split_end = s->flat.split_end;
     info->n_split_leaves = (uint32_t)s->flat.stri.size();
     info->n_split_boxes = (uint32_t)(s->flat.sboxes.size() / 8);
+    info->n_spheres = h.n_spheres;
     return RT_OK;
 }
 
@@ -626,6 +638,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     if (!c || !s) return RT_ERR_INVALID;
     if (!s->built) { c->err = "scene not built (rt_scene_build)"; return RT_ERR_STATE; }
     std::vector<float> verts;
+    if (s->flat.hdr.n_spheres > 0) { c->err = "the GPU BVH build takes triangle meshes only (the scene has spheres)"; return RT_ERR_INVALID; }
     if (!lbvh_inputs(s, verts)) { c->err = "the GPU BVH build needs >= 2 triangles"; return RT_ERR_INVALID; }
     if (s->flat.hdr.n_tris >= (1u << 30)) { c->err = "the GPU BVH build takes < 2^30 triangles (node ids are int)"; return RT_ERR_INVALID; }
     rt_status r = rt_upload_scene(c, s);   // materials, light tables, ... (the host tree is replaced below)
@@ -714,6 +727,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (!(p->flags & RT_RENDER_WHITTED) && !(p->rr >= 0.0f && p->rr < 1.0f)) { c->err = "rr must be in [0, 1)"; return RT_ERR_INVALID; }
     HIPC(c, hipSetDevice(c->device));
     const bool whitted = (p->flags & RT_RENDER_WHITTED) != 0;
+    if (whitted && c->hdr.n_spheres > 0) { c->err = "Whitted renders take triangle meshes (the path tracer's spheres: rt_scene_add_sphere)"; return RT_ERR_INVALID; }
     const bool exact = !whitted && (p->flags & RT_RENDER_EXACT) != 0, count = (p->flags & RT_RENDER_COUNT) != 0;
     if (exact) {
         // the fold stack / ring, sized from rr (reallocated when a render needs more levels)
@@ -824,6 +838,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     // ADVICE r04/r05)
     const uint32_t bvh_block = [&]() -> uint32_t {
         if (count || c->gb_next) return RT_KERNEL_REASON_MODE;
+        if (c->hdr.n_spheres > 0) return RT_KERNEL_REASON_SPHERES;   // the vertex kernel's leaves are triangles
         if (!c->vertex || !c->vertex_bvh) return RT_KERNEL_REASON_KNOB;
         if (P.n_tris >= (1u << 31)) return RT_KERNEL_REASON_TRIANGLES;
         if (P.n_mats >= (1u << 14)) return RT_KERNEL_REASON_MATERIALS;
@@ -1101,6 +1116,7 @@ rt_status rt_render_denoised(rt_ctx* c, const rt_camera* cam, const float proj[1
 {
     if (!c || !cam || !proj || !view || !dp) return RT_ERR_INVALID;
     if (!c->has_scene || c->hdr.n_nodes == 0) { c->err = "no triangle scene uploaded"; return RT_ERR_STATE; }
+    if (c->hdr.n_spheres > 0) { c->err = "the Denoiser project's G-buffer takes triangle meshes (the scene has spheres)"; return RT_ERR_INVALID; }
     if (!c->d_accum) { c->err = "no viewport (rt_resize)"; return RT_ERR_STATE; }
     if (c->nranks != 1) { c->err = "the denoiser filters whole frames: rt_resize with nranks == 1"; return RT_ERR_INVALID; }
     if (frame == 0) { c->err = "frame is 1-based"; return RT_ERR_INVALID; }

@@ -365,6 +365,37 @@ __device__ __forceinline__ bool moller_trumbore(const V3& a, const V3& e1, const
     return moller_trumbore_od(a, e1, e2, r.o, r.d, t_out);
 }
 
+// Whitted::Sphere::GetIntersectionRecord (MC/Sphere.h:62-97) by Whitted::QuadraticFormula (MC/WhittedUtilities.h:36-60):
+// A = dot(d, d), B = 2 dot(d, o - c), C = dot(o - c, o - c) - r^2 and the discriminant B*B - (4*A)*C in float; a
+// double root -0.5*B/A and q = -0.5*(B +- sqrt(disc)) in double (the reference's double literal), each rounded to
+// float as the reference assigns it; x_small = q/A, x_large = C/q in float, ordered; the nearer root unless it is
+// negative, then the farther; no hit when both are.  A NaN root (only from non-finite operands) is no hit: the
+// reference would return a record with t = NaN, which its t comparisons then order inconsistently.
+__device__ __forceinline__ bool sphere_hit(const V3& c, float r2, const Ray& r, double& t_out)
+{
+    const V3 co = sub(r.o, c);
+    const float A = dot(r.d, r.d);
+    const float B = 2.0f * dot(r.d, co);
+    const float C = dot(co, co) - r2;
+    const float disc = B * B - (4.0f * A) * C;
+    if (disc < 0.0f) return false;
+    float xs, xl;
+    if (disc == 0.0f) {
+        xl = (float)((-0.5 * (double)B) / (double)A);
+        xs = xl;
+    } else {
+        const float sq = __builtin_sqrtf(disc);
+        const float q = (B > 0.0f) ? (float)(-0.5 * (double)(B + sq)) : (float)(-0.5 * (double)(B - sq));
+        xs = q / A;
+        xl = C / q;
+    }
+    if (xs > xl) { const float tmp = xs; xs = xl; xl = tmp; }
+    if (xs < 0.0f) xs = xl;
+    if (xs < 0.0f || xs != xs) return false;
+    t_out = (double)xs;
+    return true;
+}
+
 // ------------------------------------------------------------------------------ packed f32
 // two floats in the halves of a register pair: v_pk_mul_f32 / v_pk_add_f32 round each half exactly like
 // the scalar instruction, at half the issue cost

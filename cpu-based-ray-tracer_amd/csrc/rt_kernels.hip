@@ -200,10 +200,9 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                 if (!finished) {
                     // ------------ shading, first half (MC/Renderer.cpp:163-186): shading point, light
                     // sample, shadow ray set-up
-                    const float4 tq3 = S.tris[4 * ttri + 3];
                     const V3 wo = neg(ray.d);
                     const V3 loc = add(ray.o, smul((float)tbest, ray.d));   // Ray::operator(), MC/Ray.h:34-37
-                    const V3 N{tq3.x, tq3.y, tq3.z};
+                    const V3 N = leaf_normal(S, ttri, loc);
                     const V3 n = (dot(N, wo) < 0.0f) ? neg(N) : N;
                     const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
                     st3(LS_SN, n);
@@ -498,9 +497,8 @@ __global__ void __launch_bounds__(256, RT_MIN_WAVES) pt_megakernel(KParams P)
                     const int parked = slot == 0 ? parked0 : parked1;
                     if (parked < 0 || toccl) continue;
                     if (COUNT) { ++tri_tests; if (lane == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1)) ++w_mt; }
-                    const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
                     double t;
-                    if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, ray, t)) {
+                    if (leaf_hit(S, parked, ray, t)) {
                         if (shadow) {
                             // not occluded iff length(q-p) < t + 0.01f for every hit (MC/Renderer.cpp:184)
                             if (!(slen < t + (double)0.01f)) { toccl = true; ti = NN; }

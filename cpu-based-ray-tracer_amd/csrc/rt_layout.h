@@ -18,6 +18,9 @@
 //              q0 = (a.xyz, bits(material)), q1 = (e1 = b-a, bits(primitive id)), q2 = (e2 = c-a, 0), q3 = (n.xyz, 0)
 //            (primitive id: 1 + creation index over all meshes, the Denoiser's G-buffer id, DN/TriangleMesh.h:54-62)
 //            (Moller-Trumbore reads q0..q2 = 48 B; shading reads q3)
+//            a sphere slot (Whitted::Sphere, MC/Sphere.h:16-108; round 6): q0 = (center.xyz, bits(material)),
+//            q1 = (radius^2, radius, 0, bits(primitive id)), q2 = (0, 0, 0, bits(1): the sphere flag), q3 = 0
+//            (the normal is normalize(location - center) at the hit)
 //  mats    : 2 x float4 per material: (brdf = albedo/PI, emitting), (emission, 0)
 //  lnodes  : light-mesh BVH for area sampling (BVH::Sampling_from_node, MC/BVH.h:114-129):
 //            1 x float4 per node (area, bits(left), bits(right), bits(light_tri)), root = 0
@@ -58,6 +61,7 @@ typedef struct {
     uint32_t n_lboxes;         // distinct leaf boxes of a small scene (<= 64 triangles), 0 otherwise
     uint32_t has_qnodes;       // the compact BVH below was built (every leaf box is its triangle's vertex box)
     float q_origin[3], q_scale[3];   // compact BVH plane decode: plane = fmaf((float)q, scale, origin)
+    uint32_t n_spheres;        // sphere entities (their slots in `tris` carry the sphere flag)
 } rt_scene_header;
 
 // Compact BVH (the vertex kernel's BVH variant; rays with a finite reciprocal direction):

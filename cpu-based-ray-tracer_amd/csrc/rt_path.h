@@ -62,6 +62,27 @@ struct SceneView {
     const float4* lboxes;   // small scenes: distinct leaf boxes (rt_layout.h), else unused
 };
 
+// A leaf's primitive: Moller-Trumbore on a triangle slot, the sphere quadratic on a sphere slot (the flag in
+// q2.w, rt_layout.h; scenes with spheres render on the megakernel)
+__device__ __forceinline__ bool leaf_hit(const SceneView& S, int slot, const Ray& r, double& t)
+{
+    const float4 t0 = S.tris[4 * slot], t1 = S.tris[4 * slot + 1], t2 = S.tris[4 * slot + 2];
+    if (__float_as_uint(t2.w) != 0u) return sphere_hit(V3{t0.x, t0.y, t0.z}, t1.x, r, t);
+    return moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t);
+}
+// the surface normal of a hit at `loc`: a triangle's face normal (q3), a sphere's Whitted::normalize(loc - center)
+// (MC/Sphere.h:94)
+__device__ __forceinline__ V3 leaf_normal(const SceneView& S, int slot, const V3& loc)
+{
+    const float4 t2 = S.tris[4 * slot + 2];
+    if (__float_as_uint(t2.w) != 0u) {
+        const float4 t0 = S.tris[4 * slot];
+        return w_normalize(sub(loc, V3{t0.x, t0.y, t0.z}));
+    }
+    const float4 t3 = S.tris[4 * slot + 3];
+    return V3{t3.x, t3.y, t3.z};
+}
+
 // One traversal: closest hit (shadow == false) or any blocking hit (shadow == true).
 // Leaf triangles are postponed: a lane that reaches a leaf whose box it hits parks the triangle and
 // the wave keeps walking boxes until every lane has a parked triangle or has finished; then all
@@ -89,9 +110,8 @@ __device__ __forceinline__ void traverse_impl(const SceneView& S, const Ray& r, 
         }
         if (parked >= 0) {
             if (COUNT) ++tri_tests;
-            const float4 t0 = S.tris[4 * parked], t1 = S.tris[4 * parked + 1], t2 = S.tris[4 * parked + 2];
             double t;
-            if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
+            if (leaf_hit(S, parked, r, t)) {
                 if (shadow) {
                     // not occluded iff length(q-p) < t + 0.01f for every hit (MC/Renderer.cpp:184)
                     if (!(slen < t + (double)0.01f)) { occluded = true; i = n; }

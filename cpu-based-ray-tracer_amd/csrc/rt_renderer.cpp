@@ -209,13 +209,14 @@ struct Renderer::Impl {
     // the queries' context: ctx, or (several devices) one on the first device holding the scene
     rt_ctx* qctx = nullptr;
     bool qctx_stale = true;
-    std::vector<float> tri_normal;    // per flattened triangle: face normal (rt_scene_export)
-    std::vector<int32_t> tri_mesh;    // per flattened triangle: mesh index
+    std::vector<float> tri_normal;    // per flattened slot: a triangle's face normal, a sphere's center (rt_scene_export)
+    std::vector<int32_t> tri_mesh;    // per flattened slot: entity index
+    std::vector<uint8_t> tri_sphere;  // per flattened slot: a sphere
 
-    void check(rt_status s, const char* what) const
+    void check(rt_status s, const std::string& what) const
     {
         if (s != RT_OK)
-            throw rt::Error(std::string(what) + " failed (" + std::to_string(s) + "): " + (group ? rt_group_last_error(group) : rt_last_error(ctx)));
+            throw rt::Error(what + " failed (" + std::to_string(s) + "): " + (group ? rt_group_last_error(group) : rt_last_error(ctx)));
     }
     rt_ctx* query_ctx()
     {
@@ -278,13 +279,27 @@ void Renderer::GenerateBVH()
     Impl& I = *impl_;
     rt_scene* sc = nullptr;
     I.check(rt_scene_create(&sc), "rt_scene_create");
-    for (rt::Entity* e : entities) {
-        const auto& raw = e->RawPositions();
+    for (size_t k = 0; k < entities.size(); ++k) {
+        rt::Entity* e = entities[k];
         const rt::Material& m = e->GetMaterial();
         const float alb[3] = {m.diffuse_coefficient.x, m.diffuse_coefficient.y, m.diffuse_coefficient.z};
         const float em[3] = {m.emission.x, m.emission.y, m.emission.z};
-        rt_status st = rt_scene_add_mesh(sc, raw.data(), raw.size() / 9, alb, em, nullptr);
-        if (st != RT_OK) { rt_scene_destroy(sc); I.check(st, "rt_scene_add_mesh"); }
+        vec3 c{};
+        float r = 0.0f;
+        rt_status st;
+        if (e->SphereShape(c, r)) {   // Whitted::Sphere (MC/Sphere.h:16-108)
+            const float cc[3] = {c.x, c.y, c.z};
+            st = rt_scene_add_sphere(sc, cc, r, alb, em, nullptr);
+        } else {
+            const auto& raw = e->RawPositions();
+            if (raw.size() < 9) {
+                rt_scene_destroy(sc);
+                throw rt::Error("GenerateBVH: entity " + std::to_string(k) + " is neither a triangle mesh nor a sphere: a "
+                                "user-defined shape has no device form (the path kernels intersect triangles and spheres)");
+            }
+            st = rt_scene_add_mesh(sc, raw.data(), raw.size() / 9, alb, em, nullptr);
+        }
+        if (st != RT_OK) { rt_scene_destroy(sc); I.check(st, "GenerateBVH (entity " + std::to_string(k) + ")"); }
     }
     rt_status st = rt_scene_build(sc);
     if (st == RT_OK) st = I.group ? rt_group_upload_scene(I.group, sc) : rt_upload_scene(I.ctx, sc);
@@ -301,8 +316,10 @@ void Renderer::GenerateBVH()
     I.check(rt_scene_export(sc, nf.data(), ni.data(), tf.data(), ti.data()), "rt_scene_export");
     I.tri_normal.resize((size_t)info.n_tris * 3);
     I.tri_mesh.resize(info.n_tris);
+    I.tri_sphere.resize(info.n_tris);
     for (size_t i = 0; i < info.n_tris; ++i) {
-        for (int k = 0; k < 3; ++k) I.tri_normal[3 * i + k] = tf[13 * i + 9 + k];
+        I.tri_sphere[i] = ti[2 * i + 1] == -2 ? 1 : 0;   // a sphere's slot: tri_f a = its center (rt_capi.h)
+        for (int k = 0; k < 3; ++k) I.tri_normal[3 * i + k] = tf[13 * i + (I.tri_sphere[i] ? 0 : 9) + k];
         I.tri_mesh[i] = ti[2 * i];
     }
 }
@@ -320,7 +337,19 @@ Renderer::Hit Renderer::Trace(const vec3& origin, const vec3& direction) const
     Hit h;
     if (tri >= 0 && (size_t)tri < I.tri_mesh.size()) {
         h.hit = true; h.t = t; h.triangle = tri; h.mesh = I.tri_mesh[tri];
-        h.normal = vec3{I.tri_normal[3 * tri], I.tri_normal[3 * tri + 1], I.tri_normal[3 * tri + 2]};
+        const float* q = &I.tri_normal[3 * (size_t)tri];
+        if (I.tri_sphere[tri]) {
+            // Sphere::GetIntersectionRecord (MC/Sphere.h:92-94): location = ray((float)t), normal =
+            // Whitted::normalize(location - center) (MC/VectorFloat.h:22-31), in float as the reference
+            const float tf32 = (float)t;
+            const float lx = origin.x + tf32 * direction.x, ly = origin.y + tf32 * direction.y, lz = origin.z + tf32 * direction.z;
+            const float vx = lx - q[0], vy = ly - q[1], vz = lz - q[2];
+            const float l2 = vx * vx + vy * vy + vz * vz;
+            if (l2 > 0) { const float inv = 1 / std::sqrt(l2); h.normal = vec3{vx * inv, vy * inv, vz * inv}; }
+            else h.normal = vec3{vx, vy, vz};
+        } else {
+            h.normal = vec3{q[0], q[1], q[2]};
+        }
     }
     return h;
 }

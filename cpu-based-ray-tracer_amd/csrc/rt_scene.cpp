@@ -47,6 +47,9 @@ struct Tri {
     Box box;
     int mesh;
     int id;   // primitive id: 1 + creation index over all meshes (DN/TriangleMesh.h:54-62, DN/Renderer.cpp:36-43)
+    // a sphere entity's one slot (a = its center): radius and radius_squared (MC/Sphere.h:19-23)
+    bool sphere = false;
+    float radius = 0.0f, r2 = 0.0f;
 };
 
 // A built (unflattened) binary tree; leaves reference an item id.
@@ -319,6 +322,17 @@ std::vector<MeshDesc> SceneBuilder::cornell_box_meshes()
     return out;
 }
 
+int SceneBuilder::add_sphere(const F3& center, float radius, const MaterialDesc& m)
+{
+    MeshDesc d;
+    d.sphere = true;
+    d.center = center;
+    d.radius = radius;
+    d.material = m;
+    d.name = "sphere" + std::to_string(meshes_.size());
+    return add_mesh(std::move(d));
+}
+
 int SceneBuilder::add_mesh(MeshDesc m)
 {
     meshes_.push_back(std::move(m));
@@ -416,7 +430,31 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     std::vector<Box> mesh_box(nm);
     std::vector<float> mesh_area(nm, 0.0f);
     int id_count = 1;
+    uint32_t n_spheres = 0;
     for (size_t mi = 0; mi < nm; ++mi) {
+        if (meshes_[mi].sphere) {
+            // Whitted::Sphere (MC/Sphere.h:19-23,45-48): radius_squared = r * r, surface_area = 4 * PI * r^2 (4 * PI
+            // first, a float), Get3DAABB = AABB_3D{center + r, center - r} (componentwise std::fmin / std::fmax,
+            // MC/BoundingVolume.h:47-51); a top-level leaf of the entity BVH with one sphere slot
+            const MeshDesc& d = meshes_[mi];
+            const float PI = 3.141592653589793f;   // MC/WhittedUtilities.h:20
+            Tri tr{};
+            tr.sphere = true;
+            tr.a = d.center; tr.radius = d.radius; tr.r2 = d.radius * d.radius;
+            tr.area = 4 * PI * tr.r2;
+            const F3 p1{d.center.x + d.radius, d.center.y + d.radius, d.center.z + d.radius};
+            const F3 p2{d.center.x - d.radius, d.center.y - d.radius, d.center.z - d.radius};
+            tr.box = Box{F3{std::fmin(p1.x, p2.x), std::fmin(p1.y, p2.y), std::fmin(p1.z, p2.z)},
+                         F3{std::fmax(p1.x, p2.x), std::fmax(p1.y, p2.y), std::fmax(p1.z, p2.z)}};
+            tr.mesh = (int)mi; tr.id = id_count++;
+            tris[mi].push_back(tr);
+            mesh_box[mi] = tr.box;
+            mesh_area[mi] = tr.area;
+            mesh_nodes[mi].push_back(BNode{tr.box, tr.area, -1, -1, 0});
+            mesh_root[mi] = 0;
+            ++n_spheres;
+            continue;
+        }
         const auto& raw = meshes_[mi].raw;
         const size_t nt = raw.size() / 9;
         if (nt == 0) { err = "mesh without triangles: " + meshes_[mi].name; return false; }
@@ -527,7 +565,9 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     // Triangles with identical leaf boxes (the two halves of a quad) share one test.
     out.lboxes.clear();
     out.hdr.n_lboxes = 0;
-    if (NT > 0 && NT <= 64) {
+    // (scenes with spheres render on the megakernel's BVH walk: no leaf-box trace, split trace, near-first
+    // orderings, compact BVH or light-plane masks, which are all built for triangle leaves)
+    if (NT > 0 && NT <= 64 && n_spheres == 0) {
         bool contained = true;
         std::vector<std::pair<Box, uint64_t>> uniq;
         for (uint32_t i = 0; i < NN && contained; ++i) {
@@ -629,7 +669,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     out.wcopies.clear();
     out.stri.clear();
     out.split_root = out.split_end = 0;
-    if (NT > 64) {
+    if (NT > 64 && n_spheres == 0) {
         std::vector<uint32_t> leaf_pre(NN + 1, 0);   // leaves among nodes [0, i)
         for (uint32_t i = 0; i < NN; ++i) leaf_pre[i + 1] = leaf_pre[i] + (fn[i].tri >= 0 ? 1u : 0u);
         const uint32_t n_leaves = leaf_pre[NN];
@@ -684,7 +724,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     // contains a leaf box), so for a finite ray a leaf's own slab test decides whether the reference reaches
     // it and any pre-order of any tree over the same leaf boxes visits the same candidates
     out.worders.clear();
-    if (!lights_.empty() && NT > 64) {
+    if (!lights_.empty() && NT > 64 && n_spheres == 0) {
         bool nested = true;
         auto inside = [](const Box& a, const Box& b) {   // b inside a
             return a.lo.x <= b.lo.x && a.lo.y <= b.lo.y && a.lo.z <= b.lo.z && a.hi.x >= b.hi.x && a.hi.y >= b.hi.y && a.hi.z >= b.hi.z;
@@ -698,6 +738,19 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     out.dbg_tri_i.resize((size_t)NT * 2);
     for (uint32_t s = 0; s < NT; ++s) {
         const Tri& t = *slot_tri[s];
+        if (t.sphere) {   // rt_layout.h: (center, material)(r^2, r, 0, id)(0, 0, 0, bits(1))(0)
+            float* q = &out.tris[16 * (size_t)s];
+            q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = bits_as_float(t.mesh);
+            q[4] = t.r2; q[5] = t.radius; q[6] = 0.0f; q[7] = bits_as_float(t.id);
+            q[8] = q[9] = q[10] = 0.0f; q[11] = bits_as_float(1);
+            q[12] = q[13] = q[14] = q[15] = 0.0f;
+            float* d = &out.dbg_tri_f[13 * (size_t)s];
+            d[0] = t.a.x; d[1] = t.a.y; d[2] = t.a.z; d[3] = t.radius; d[4] = t.r2;
+            for (int k = 5; k < 12; ++k) d[k] = 0.0f;
+            d[12] = t.area;
+            out.dbg_tri_i[2 * s] = t.mesh; out.dbg_tri_i[2 * s + 1] = -2;
+            continue;
+        }
         const F3 e1 = sub(t.b, t.a), e2 = sub(t.c, t.a);
         float* q = &out.tris[16 * (size_t)s];
         q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = bits_as_float(t.mesh);   // material id == mesh id
@@ -719,7 +772,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     // tests -- exact -- select exactly the reference's candidate triangles.
     out.qnodes.clear(); out.tabc.clear(); out.tnrm.clear();
     out.hdr.has_qnodes = 0;
-    if (NN > 0 && NT > 0) {
+    if (NN > 0 && NT > 0 && n_spheres == 0) {
         const Box& root = fn[0].box;
         const float lo3[3] = {root.lo.x, root.lo.y, root.lo.z}, hi3[3] = {root.hi.x, root.hi.y, root.hi.z};
         float org[3], scl[3];
@@ -795,7 +848,14 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     for (size_t mi = 0; mi < nm; ++mi) {
         const MaterialDesc& m = meshes_[mi].material;
         const bool emitting = std::sqrt(dot(m.emission, m.emission)) > 0.00001f;   // MC/WhittedMaterial.h:34
-        if (emitting && light < 0) light = (int)mi;
+        if (emitting && light < 0) {
+            if (meshes_[mi].sphere) {
+                // SamplingAreaLight would call Sphere::Sampling, which sets nothing (a TODO, MC/Sphere.h:30-33)
+                err = "the first emissive entity is a sphere: the reference's Sphere::Sampling is unimplemented";
+                return false;
+            }
+            light = (int)mi;
+        }
         float* q = &out.mats[8 * mi];
         q[0] = m.albedo.x / PI; q[1] = m.albedo.y / PI; q[2] = m.albedo.z / PI; q[3] = emitting ? 1.0f : 0.0f;
         q[4] = m.emission.x; q[5] = m.emission.y; q[6] = m.emission.z; q[7] = 0.0f;
@@ -860,7 +920,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         // A split scene (larger scenes, <= 32 leaves outside the walked subtree) gets the same masks over its
         // outside slots: the kernel's split phase tests those leaves like the narrow build's triangles.
         const bool split_masks = NT > 32 && !out.stri.empty();
-        if (NT <= 32 || split_masks) {
+        if ((NT <= 32 || split_masks) && n_spheres == 0) {
             double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
             auto vert = [&](uint32_t s, int k, double v[3]) {
                 const float* q = &out.tris[16 * (size_t)s];
@@ -919,6 +979,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     out.hdr.n_nodes = NN; out.hdr.n_tris = NT; out.hdr.n_mats = (uint32_t)nm;
     out.hdr.n_lnodes = (uint32_t)(out.lnodes.size() / 4); out.hdr.n_ltris = (uint32_t)(out.ltris.size() / 16);
     out.hdr.max_depth = depth;
+    out.hdr.n_spheres = n_spheres;
     return true;
 }
 

@@ -24,6 +24,10 @@ struct MeshDesc {
     float scale = 0.01f;
     bool has_offset = false;
     F3 offset{0.0f, 0.0f, 0.0f};
+    // a sphere entity of the path-traced scene instead of a mesh (Whitted::Sphere, MC/Sphere.h:16-108): raw is empty
+    bool sphere = false;
+    F3 center{0.0f, 0.0f, 0.0f};
+    float radius = 0.0f;
 };
 
 struct PointLight { F3 position; F3 radiance; };
@@ -81,6 +85,8 @@ public:
     void add_cornell_box();
     static std::vector<MeshDesc> cornell_box_meshes();
     int add_mesh(MeshDesc m);
+    // Renderer::Add(new Whitted::Sphere(center, radius, material)) (MC/Sphere.h:19-23): an entity like a mesh
+    int add_sphere(const F3& center, float radius, const MaterialDesc& m);
     // Renderer::Add(std::unique_ptr<PointLightSource>), BV/Renderer.h:88-97
     void add_point_light(const PointLight& l) { lights_.push_back(l); }
     void set_sky(const F3& c) { sky_ = c; }

@@ -19,7 +19,7 @@
 #include <cstdint>
 #include <stdexcept>
 
-#define RT_CXX_ABI_VERSION 1
+#define RT_CXX_ABI_VERSION 2   /* 2 (round 6): rt::Entity gained SphereShape, rt::Sphere */
 
 namespace rt {
 

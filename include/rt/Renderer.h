@@ -26,11 +26,27 @@ struct Material {   // Whitted::WhittedMaterial (Diffuse only), MC/WhittedMateri
     vec3 emission{0.0f, 0.0f, 0.0f};
 };
 
-class Entity {   // Whitted::Entity (MC/Entity.h:19-55): here only triangle meshes exist
+// The device's view of an entity (Whitted::Entity, MC/Entity.h:19-55), read by Renderer::GenerateBVH: a triangle
+// mesh's objl positions (pre-scale), or a sphere's center and radius, and the material.  An entity that is
+// neither (a user-defined shape: its intersection code runs on the host in the reference) has no device form, and
+// GenerateBVH throws rt::Error for it.
+class Entity {
 public:
     virtual ~Entity() = default;
-    virtual const std::vector<float>& RawPositions() const = 0;   // objl positions, pre-scale
-    virtual const Material& GetMaterial() const = 0;
+    virtual const std::vector<float>& RawPositions() const { static const std::vector<float> none; return none; }
+    virtual bool SphereShape(vec3& center, float& radius) const { (void)center; (void)radius; return false; }
+    virtual const Material& GetMaterial() const { static const Material none; return none; }
+};
+
+class Sphere : public Entity {   // Whitted::Sphere(center, radius, material), MC/Sphere.h:16-108
+public:
+    Sphere(const vec3& center, float radius, const Material& m) : center_(center), radius_(radius), material_(m) {}
+    bool SphereShape(vec3& center, float& radius) const override { center = center_; radius = radius_; return true; }
+    const Material& GetMaterial() const override { return material_; }
+private:
+    vec3 center_;
+    float radius_;
+    Material material_;
 };
 
 class TriangleMesh : public Entity {   // Whitted::TriangleMesh(file_path, material), MC/TriangleMesh.h:148-186

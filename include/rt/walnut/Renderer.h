@@ -19,7 +19,8 @@
 #include "Walnut/Image.h"
 #include "Camera.h"
 #include "Ray.h"       // AccelerationStructure::Ray, as MC/Renderer.h brings it
-#include "Whitted.h"   // Whitted::TriangleMesh / WhittedMaterial / Entity / IntersectionRecord, as MC/Renderer.h brings them
+#include "Whitted.h"   // Whitted::TriangleMesh / Sphere / WhittedMaterial / Entity / IntersectionRecord, as MC/Renderer.h brings them
+#include "BVH.h"       // AccelerationStructure::BVH (the public `bvh` member)
 #include "../Renderer.h"
 
 // Average indices of refraction, MC/Renderer.h:22-28
@@ -36,8 +37,8 @@ class Renderer {
 public:
     using Settings = rt::Renderer::Settings;   // Settings::accumulating, MC/Renderer.h:34-37
 
-    // the Cornell box (MC/Renderer.cpp:26-57): the core builds the meshes; the four materials are kept here so
-    // that hit records point at a WhittedMaterial as the reference's do
+    // the Cornell box (MC/Renderer.cpp:26-57): six Whitted::TriangleMesh entities over the core's built-in
+    // Cornell positions and the reference's four materials, then GenerateBVH
     Renderer()
     {
         auto mk = [](glm::vec3 emission, glm::vec3 albedo) {
@@ -51,8 +52,15 @@ public:
         builtin_materials_.push_back(mk(glm::vec3{47.8f, 38.6f, 31.1f}, glm::vec3{0.7f, 0.7f, 0.7f}));    // light
         // floor, shortbox, tallbox: white; left: red; right: green; light (MC/Renderer.cpp:36-41)
         const int which[6] = {2, 2, 2, 0, 1, 3};
-        for (int k : which) builtin_mesh_material_.push_back(builtin_materials_[k].get());
+        const std::vector<rt::Entity*> cornell = core_.GetEntities();
+        for (size_t k = 0; k < cornell.size() && k < 6; ++k) {
+            builtin_meshes_.push_back(std::make_unique<Whitted::TriangleMesh>(cornell[k]->RawPositions(), builtin_materials_[which[k]].get()));
+            Add(builtin_meshes_.back().get());
+        }
+        GenerateBVH();
     }
+    Renderer(const Renderer&) = delete;
+    Renderer& operator=(const Renderer&) = delete;
 
     // MC/Renderer.cpp:59-89: the Walnut image is created once and resized with the viewport
     void ResizeViewport(uint32_t width, uint32_t height)
@@ -76,10 +84,29 @@ public:
     void Reaccumulate() { core_.Reaccumulate(); }
     uint32_t GetSPP() { return core_.GetSPP(); }
     Settings& GetSettings() { return core_.GetSettings(); }
-    // the scene-extension API, MC/Renderer.h:72-86: Add(new Whitted::TriangleMesh(path, material)) then GenerateBVH()
-    [[nodiscard]] const std::vector<Whitted::Entity*>& GetEntities() const { return core_.GetEntities(); }
-    void Add(Whitted::Entity* entity_pointer) { core_.Add(entity_pointer); }
-    void GenerateBVH() { core_.GenerateBVH(); }
+    // the scene-extension API, MC/Renderer.h:72-86: Add(new Whitted::TriangleMesh(path, material)) or
+    // Add(new Whitted::Sphere(center, radius, material)), then GenerateBVH(), which builds the device scene from
+    // `entities` (a user-defined Whitted::Entity has no device form: rt::Error)
+    [[nodiscard]] const std::vector<Whitted::Entity*>& GetEntities() const { return entities; }
+    void Add(Whitted::Entity* entity_pointer) { entities.push_back(entity_pointer); }
+    void GenerateBVH()
+    {
+        core_.entities.assign(entities.begin(), entities.end());
+        core_.GenerateBVH();
+        bvh_.reset(new AccelerationStructure::BVH([this](const AccelerationStructure::Ray& r) { return ray_BVH_intersection_record(r); }));
+        bvh = bvh_.get();
+        // TriangleMesh::Sampling of the light -- the first emissive entity, the one SamplingAreaLight samples
+        // (MC/Renderer.h:169-179) -- runs the device's light sampler
+        for (Whitted::Entity* e : entities) {
+            if (auto* t = dynamic_cast<Whitted::TriangleMesh*>(e)) t->light_sampler = nullptr;
+        }
+        for (Whitted::Entity* e : entities) {
+            if (!e->IsEmissive()) continue;
+            if (auto* t = dynamic_cast<Whitted::TriangleMesh*>(e))
+                t->light_sampler = [this](Whitted::IntersectionRecord& rec, float& pdf) { SamplingAreaLight(rec, pdf); };
+            break;
+        }
+    }
 
     // Renderer::ray_BVH_intersection_record (MC/Renderer.h:88-91): the closest hit of the ray in the scene of
     // the last GenerateBVH -- the device traversal (rt_trace), the reference's double t and tie rule -- filled
@@ -172,36 +199,37 @@ public:
     }
 
     float RR_survival_probability = 0.8f;   // MC/Renderer.h:199 (read at every Render)
+    AccelerationStructure::BVH* bvh = nullptr;   // MC/Renderer.h:200: the scene of the last GenerateBVH
+    std::vector<Whitted::Entity*> entities;      // MC/Renderer.h:201: what GenerateBVH builds the scene from
 
     rt::Renderer& Core() { return core_; }
 
 private:
     static float dot(const glm::vec3& a, const glm::vec3& b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }   // glm's order
     Whitted::Entity* entity_of(int32_t mesh) const
-    {
+    {   // the entities of the last GenerateBVH, in Add order
         const auto& e = core_.GetEntities();
-        return mesh >= 0 && (size_t)mesh < e.size() ? e[mesh] : nullptr;
+        return mesh >= 0 && (size_t)mesh < e.size() ? dynamic_cast<Whitted::Entity*>(e[mesh]) : nullptr;
     }
     Whitted::WhittedMaterial* material_of(int32_t mesh) const
     {
         Whitted::Entity* e = entity_of(mesh);
         if (auto* t = dynamic_cast<Whitted::TriangleMesh*>(e)) return t->UnifiedMaterial();
-        // the constructor's Cornell meshes (the first six entities, unless the caller replaced them)
-        return mesh >= 0 && (size_t)mesh < builtin_mesh_material_.size() && !dynamic_cast<Whitted::TriangleMesh*>(e) ? builtin_mesh_material_[mesh] : nullptr;
+        if (auto* sp = dynamic_cast<Whitted::Sphere*>(e)) return sp->UnifiedMaterial();
+        return nullptr;
     }
     bool has_light() const
-    {   // IsEmissive of some entity: length(emission) > 1e-5 (MC/WhittedMaterial.h:34)
-        for (Whitted::Entity* e : core_.GetEntities()) {
-            const rt::vec3 m = e->GetMaterial().emission;
-            if (std::sqrt((m.x * m.x + m.y * m.y) + m.z * m.z) > 0.00001f) return true;
-        }
+    {   // IsEmissive of some entity of the scene (MC/Renderer.h:169-179)
+        for (rt::Entity* e : core_.GetEntities())
+            if (auto* w = dynamic_cast<Whitted::Entity*>(e); w && w->IsEmissive()) return true;
         return false;
     }
 
     rt::Renderer core_;
     std::shared_ptr<Walnut::Image> frame_image_final;
     std::vector<std::unique_ptr<Whitted::WhittedMaterial>> builtin_materials_;
-    std::vector<Whitted::WhittedMaterial*> builtin_mesh_material_;
+    std::vector<std::unique_ptr<Whitted::TriangleMesh>> builtin_meshes_;
+    std::unique_ptr<AccelerationStructure::BVH> bvh_;
 };
 
 #endif

@@ -35,8 +35,9 @@ extern "C" {
 #endif
 
 /* 2 (round 4): rt_stats grew last_prepass_ms / last_main_ms, rt_scene_info the light-skip and split fields,
- * rt_read_accumulation was added; a host built against another version must not pass its structs */
-#define RT_API_VERSION 3
+ * rt_read_accumulation was added; a host built against another version must not pass its structs
+ * 4 (round 6): rt_scene_add_sphere, rt_scene_info.n_spheres, RT_KERNEL_REASON_SPHERES */
+#define RT_API_VERSION 4
 
 typedef int32_t rt_status;
 #define RT_OK 0
@@ -98,6 +99,15 @@ rt_status rt_scene_add_world_mesh(rt_scene* s, const float* vertices, uint32_t n
                                   const float* uv, const rt_world_material* m, int32_t* entity_id);
 /* Renderer::Renderer() of the Whitted Style Ray Tracer: diffuse + glass sphere, chessboard, two lights */
 rt_status rt_scene_add_two_spheres_scene(rt_scene* s);
+/* Whitted::Sphere(center, radius, material) + Renderer::Add (MC/Sphere.h:16-108, MC/Renderer.h:78-81): a sphere
+ * entity of the PATH-TRACED scene (beside the triangle meshes; id = its entity index, the order of Add).  It is
+ * a top-level leaf of the entity BVH with box AABB_3D{center + radius, center - radius} and area 4 PI radius^2;
+ * rays meet it by the reference's float QuadraticFormula (MC/WhittedUtilities.h:36-60, MC/Sphere.h:62-97).  An
+ * emissive sphere may not be the first emissive entity: the reference's Sphere::Sampling is empty (a TODO,
+ * MC/Sphere.h:30-33), so SamplingAreaLight would read an unset record (rt_scene_build: RT_ERR_INVALID).  Scenes
+ * with spheres render on the megakernel (rt_stats.kernel_reason RT_KERNEL_REASON_SPHERES). */
+rt_status rt_scene_add_sphere(rt_scene* s, const float center[3], float radius, const float albedo[3], const float emission[3],
+                              int32_t* entity_id);
 rt_status rt_scene_build(rt_scene* s);
 
 typedef struct {
@@ -113,6 +123,8 @@ typedef struct {
     uint32_t split_end;
     uint32_t n_split_leaves;   /* leaves outside that subtree, tested by their boxes (<= 32) */
     uint32_t n_split_boxes;    /* their distinct boxes */
+    uint32_t n_spheres;        /* sphere entities (API 4); rt_scene_export: a sphere's slot has tri_f a = center,
+                                  b = (radius, radius^2, 0), c = n = 0, area = its area, tri_i = (entity, -2) */
 } rt_scene_info;
 rt_status rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 /* flattened DFS pre-order view for tests: node_f 7/node (min[3] max[3] mesh_area), node_i 5/node
@@ -255,6 +267,7 @@ typedef struct {
 #define RT_KERNEL_REASON_MODE 3          /* megakernel: a work-counter render or a denoiser G-buffer frame */
 #define RT_KERNEL_REASON_KNOB 4          /* a debug knob (RT_VERTEX / RT_VERTEX_BVH / RT_BRUTE) chose it */
 #define RT_KERNEL_REASON_TRIANGLES 5     /* megakernel: 2^31 triangles or more (the BVH variant indexes triangles in 31 bits) */
+#define RT_KERNEL_REASON_SPHERES 6       /* megakernel: the scene has sphere entities (rt_scene_add_sphere, API 4) */
 rt_status rt_get_stats(rt_ctx* ctx, rt_stats* st);
 /* diagnostic: the raw device counters of the last rt_render (up to 512 x u64; [16..23] = wave cycles per
  * section and [24..43] = wave-level event counts of the vertex kernel in RT_SECTIONS builds, [64..511]

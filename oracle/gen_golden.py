@@ -12,6 +12,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py c1         # only the C1 (Whitted two-sphere world) fixtures
     python oracle/gen_golden.py optics     # only the Renderer optics helpers (mirror / Snell / Fresnel)
     python oracle/gen_golden.py c5         # only the C5 (Cornell + 79,488-triangle bunny) fixtures
+    python oracle/gen_golden.py spheres    # only the Cornell + Whitted::Sphere fixtures (cornell_spheres.npz)
     python oracle/gen_golden.py stat       # only the shipped-mt19937 statistical fixture
     python oracle/gen_golden.py full       # C2 and C4 at their full spp (full_c2 / full_c4: one of them)
     python oracle/gen_golden.py full_c5    # C5 (Cornell + 79k-triangle bunny) at 3840x2160x256 (~10 min)
@@ -242,6 +243,68 @@ def gen_images():
         out[f"rgba_{key}"] = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
         out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
     np.savez_compressed(os.path.join(GOLDEN, "images_cornell.npz"), **out)
+
+
+# Cornell + Whitted::Sphere entities (MC/Sphere.h:16-108 through Renderer::Add + GenerateBVH):
+# (center, radius, material of {red, green, white, light}); a white sphere on the floor, a green one above the
+# short box, a white one half inside the tall box (its surface crosses the box's faces: ties and near-ties with
+# triangles), and an emissive one (the light's material: after the light mesh, so SamplingAreaLight still picks
+# the mesh) near the ceiling
+SPHERES = [((3.9, 1.0, 1.2), 0.9, 2), ((1.5, 2.3, 1.3), 0.6, 1), ((3.4, 3.3, 3.3), 0.5, 2), ((4.6, 4.7, 4.3), 0.35, 3)]
+
+
+def sphere_extra():
+    return ",".join(f"sphere:{c[0]!r}:{c[1]!r}:{c[2]!r}:{r!r}:{m}" for (c, r, m) in SPHERES)
+
+
+def gen_spheres(rng):
+    """tests/golden/cornell_spheres.npz: the reference's own Sphere / BVH / TriangleMesh code (ref_harness) on the
+    Cornell box + SPHERES -- the flattened two-level tree, 4096 closest hits, and images at 128x128x64 (the
+    VERDICT's case) and two more shapes / roulette settings."""
+    extra = sphere_extra()
+    run("scene", CORNELL_DIR, extra, tmp("snodes"), tmp("stris"), tmp("smeshes"))
+    nodes = np.fromfile(tmp("snodes"), NODE_DT)
+    tris = np.fromfile(tmp("stris"), TRI_DT)
+    meshes = np.fromfile(tmp("smeshes"), MESH_DT)
+    cam = np.array([2.81432, 4.20749, -9.11751], np.float32)
+    lo, hi = np.array([0, 0, 0], np.float32), np.array([5.56, 5.488, 5.592], np.float32)
+    cen = np.array([c for (c, _, _) in SPHERES], np.float32)
+    rad = np.array([r for (_, r, _) in SPHERES], np.float32)
+    o, d = [], []
+    k = 1200   # camera rays into the box
+    tgt = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    o.append(np.repeat(cam[None], k, 0)); d.append(tgt - cam)
+    k = 1200   # interior origins, random directions
+    o.append(rng.uniform(lo, hi, (k, 3)).astype(np.float32)); d.append(rng.normal(size=(k, 3)).astype(np.float32))
+    k = 800    # aimed at sphere centers, from the camera and from inside the box
+    si = rng.integers(0, len(SPHERES), k)
+    src = np.where((rng.random(k) < 0.5)[:, None], cam[None], rng.uniform(lo, hi, (k, 3)).astype(np.float32))
+    o.append(src.astype(np.float32)); d.append((cen[si] - src).astype(np.float32))
+    k = 896    # grazing: aimed at points on (or just off) the silhouettes
+    si = rng.integers(0, len(SPHERES), k)
+    src = np.where((rng.random(k) < 0.5)[:, None], cam[None], rng.uniform(lo, hi, (k, 3)).astype(np.float32))
+    v = (cen[si] - src).astype(np.float32)
+    perp = np.cross(v, rng.normal(size=(k, 3)).astype(np.float32))
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True) + 1e-30
+    scale = rad[si] * rng.choice([0.999, 1.0, 1.0001, 0.5], k).astype(np.float32)
+    o.append(src.astype(np.float32)); d.append((cen[si] + perp * scale[:, None] - src).astype(np.float32))
+    o = np.concatenate(o).astype(np.float32)
+    d = np.concatenate(d).astype(np.float32)
+    np.concatenate([o, d], 1).astype("<f4").tofile(tmp("srays.in"))
+    run("rays", CORNELL_DIR, extra, tmp("srays.in"), tmp("srays.out"))
+    res = np.fromfile(tmp("srays.out"), HIT_DT)
+    out = dict(spheres_center=cen, spheres_radius=rad, spheres_material=np.array([m for (_, _, m) in SPHERES], np.int32),
+               nodes=nodes.view(np.uint8), tris=tris.view(np.uint8), meshes=meshes.view(np.uint8),
+               org=o, dir=d, hit=res["hit"], tri=res["tri"], mat=res["mat"], t=res["t"], loc=res["loc"], n=res["n"])
+    for (W, H, spp, seed, rr) in [(128, 128, 64, 0, 0.8), (96, 72, 16, 3, 0.5), (64, 48, 32, 11, 0.9)]:
+        run("image", CORNELL_DIR, extra, W, H, spp, seed, rr, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"))
+        key = f"{W}x{H}_spp{spp}_s{seed}_rr{rr}"
+        out[f"accum_{key}"] = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
+        out[f"rgba_{key}"] = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
+        out[f"stats_{key}"] = np.fromfile(tmp("stats"), "<u8")
+    np.savez_compressed(os.path.join(GOLDEN, "cornell_spheres.npz"), **out)
+    print(f"  spheres: {len(nodes)} nodes, {len(tris)} slots, {int(res['hit'].sum())} hits of {len(o)} rays, "
+          f"{int((np.isin(res['tri'], [i for i, t in enumerate(tris) if t['n'][0] == 0 and t['n'][1] == 0 and t['n'][2] == 0])).sum())} on spheres")
 
 
 FULL_CONFIGS = [("c2", 784, 784, 256), ("c4", 1920, 1080, 1024)]
@@ -664,6 +727,8 @@ def main():
             gen_dn()
         if only in ("all", "c5"):
             gen_c5(np.random.default_rng(20261016))
+        if only in ("all", "spheres"):
+            gen_spheres(np.random.default_rng(20261018))
         if only in ("all", "full", "full_c2", "full_c4"):
             gen_full(None if only in ("all", "full") else only[5:])
         if only == "full_c5":

@@ -45,6 +45,7 @@
 #include <glm/gtc/matrix_transform.hpp>
 #define private public
 #include "TriangleMesh.h"
+#include "Sphere.h"
 #include "Camera.h"
 #undef private
 #include "../philox.h"
@@ -93,6 +94,7 @@ struct Scene {
     std::map<const Whitted::Entity*, int> tri_index;   // TrianglePrimitive* -> flattened DFS leaf index
     std::map<const Whitted::WhittedMaterial*, int> mat_index;
     std::vector<int> mesh_material;
+    std::map<const Whitted::Entity*, std::array<float, 4>> sphere_def;   // Whitted::Sphere entities: center, radius
 };
 
 static Scene* build_cornell(const std::string& dir, const std::vector<std::string>& extra_objs)
@@ -115,6 +117,19 @@ static Scene* build_cornell(const std::string& dir, const std::vector<std::strin
         s->mesh_material.push_back(s->mat_index[mats[i]]);
     }
     for (const auto& p : extra_objs) {
+        if (p.rfind("sphere:", 0) == 0) {
+            // "sphere:cx:cy:cz:r:m": new Whitted::Sphere(center, radius, material m of {red, green, white, light})
+            // (MC/Sphere.h:19-23), added after the Cornell meshes like any entity (MC/Renderer.h:78-81)
+            float v[4]; int m = 2;
+            if (std::sscanf(p.c_str(), "sphere:%f:%f:%f:%f:%d", &v[0], &v[1], &v[2], &v[3], &m) != 5 || m < 0 || m > 3) {
+                fprintf(stderr, "bad sphere spec %s\n", p.c_str()); exit(2);
+            }
+            auto* sp = new Whitted::Sphere(glm::vec3{v[0], v[1], v[2]}, v[3], s->materials[m]);
+            s->entities.push_back(sp);
+            s->mesh_material.push_back(m);
+            s->sphere_def[sp] = {v[0], v[1], v[2], v[3]};
+            continue;
+        }
         s->entities.push_back(new Whitted::TriangleMesh(p, white));
         s->mesh_material.push_back(2);
     }
@@ -151,6 +166,16 @@ static void flatten_top(Scene* s, AccelerationStructure::BVH_Node* node, std::ve
     if (!node->left && !node->right) {
         auto* m = dynamic_cast<Whitted::TriangleMesh*>(node->entity);
         int mesh = (int)(std::find(s->entities.begin(), s->entities.end(), node->entity) - s->entities.begin());
+        if (!m) {   // a sphere: one leaf, one slot (a = center, b = (radius, radius^2, 0), as rt_scene_export writes it)
+            const auto& d = s->sphere_def.at(node->entity);
+            const int ti = (int)tris.size();
+            s->tri_index[node->entity] = ti;
+            tris.push_back(FlatTri{glm::vec3{d[0], d[1], d[2]}, glm::vec3{d[3], d[3] * d[3], 0.0f}, glm::vec3{0.0f}, glm::vec3{0.0f},
+                                   node->entity->GetArea(), mesh, s->mesh_material[mesh]});
+            nodes.push_back(FlatNode{node->bounding_volume.min_slab_values, node->bounding_volume.max_slab_values, node->mesh_area, -1, -1,
+                                     ti, mesh, 0});
+            return;
+        }
         // the top-level leaf box must equal the mesh-root box for the flattening to be exact
         const auto& tb = node->bounding_volume; const auto& mb = m->bvh->root->bounding_volume;
         if (tb.min_slab_values != mb.min_slab_values || tb.max_slab_values != mb.max_slab_values) { fprintf(stderr, "mesh box mismatch\n"); exit(4); }
@@ -277,9 +302,10 @@ static int cmd_scene(const char* dir, const char* extra, const char* out_nodes, 
     {
         Out o(out_meshes);   // per mesh: raw objl positions are dumped by cmd_objraw; here area/box/material
         for (size_t i = 0; i < s->entities.size(); ++i) {
-            auto* m = dynamic_cast<Whitted::TriangleMesh*>(s->entities[i]);
-            o.put(m->total_area); o.putv(m->bounding_AABB.min_slab_values); o.putv(m->bounding_AABB.max_slab_values);
-            o.put((int32_t)s->mesh_material[i]); o.put((int32_t)(m->IsEmissive() ? 1 : 0));
+            Whitted::Entity* e = s->entities[i];
+            const auto box = e->Get3DAABB();
+            o.put(e->GetArea()); o.putv(box.min_slab_values); o.putv(box.max_slab_values);
+            o.put((int32_t)s->mesh_material[i]); o.put((int32_t)(e->IsEmissive() ? 1 : 0));
         }
     }
     printf("nodes %zu tris %zu meshes %zu\n", nodes.size(), tris.size(), s->entities.size());

@@ -10,7 +10,9 @@
    (Whitted::WhittedMaterial, Whitted::TriangleMesh(path, material*), Add, GenerateBVH) against the same
    drop-in headers.  Needs no reference file.
 3. tests/walnut_stub/queries.cpp: the drop-in Renderer's scene queries and optics helpers with the reference's
-   signatures (MC/Renderer.h:88-180).  Needs no reference file."""
+   signatures (MC/Renderer.h:88-180).  Needs no reference file.
+4. tests/walnut_stub/spheres.cpp: Whitted::Sphere entities through Add / GenerateBVH and the Whitted::Entity
+   interface (MC/Entity.h:19-55, MC/Sphere.h:16-108), the public bvh / entities members.  Needs no reference file."""
 import glob
 import hashlib
 import os
@@ -23,6 +25,7 @@ MAINLOOP = "/root/reference/Monte Carlo Path Tracer/8599RayTracerGUI/src/mainloo
 BIN = os.path.join(REPO, "tests", "_bin", "walnut_mainloop")
 C5_BIN = os.path.join(REPO, "tests", "_bin", "walnut_c5_scene")
 QUERIES_BIN = os.path.join(REPO, "tests", "_bin", "walnut_queries")
+SPHERES_BIN = os.path.join(REPO, "tests", "_bin", "walnut_spheres")
 STUB = os.path.join(REPO, "tests", "walnut_stub")
 PKG = os.path.join(REPO, "cpu-based-ray-tracer_amd")
 
@@ -88,12 +91,17 @@ def build_queries(out=QUERIES_BIN):
     return _gxx([os.path.join(STUB, "queries.cpp")], out)
 
 
+def build_spheres(out=SPHERES_BIN):
+    return _gxx([os.path.join(STUB, "spheres.cpp")], out)
+
+
 def build(out=BIN, force=True):
     """Build the three binaries.  force=False rebuilds only those that are stale (missing, or older than a
     drop-in header or librt_hip.so)."""
     d = os.path.dirname(out)
     for path, fn in ((os.path.join(d, os.path.basename(C5_BIN)), build_c5),
-                     (os.path.join(d, os.path.basename(QUERIES_BIN)), build_queries)):
+                     (os.path.join(d, os.path.basename(QUERIES_BIN)), build_queries),
+                     (os.path.join(d, os.path.basename(SPHERES_BIN)), build_spheres)):
         if force or stale(path):
             fn(path)
     if not os.path.exists(MAINLOOP):

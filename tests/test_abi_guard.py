@@ -123,7 +123,9 @@ def test_settings_layout_fails_loudly(tmp_path):
 
 
 def test_abi_version_mismatch_fails_loudly(tmp_path):
-    inc = _patched_include(tmp_path, [("rt/Abi.h", "#define RT_CXX_ABI_VERSION 1\n", "#define RT_CXX_ABI_VERSION 999\n")])
+    txt = open(os.path.join(REPO, "include", "rt", "Abi.h")).read()
+    line = next(ln for ln in txt.splitlines() if ln.startswith("#define RT_CXX_ABI_VERSION "))
+    inc = _patched_include(tmp_path, [("rt/Abi.h", line + "\n", "#define RT_CXX_ABI_VERSION 999\n")])
     out = _compile_and_run(tmp_path, inc)
     for name in ("Camera", "Renderer", "DenoisingRenderer", "WhittedRenderer"):
         outcome, past, what = out[name]

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     assert len(names) >= 25
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
-    assert L.rt_api_version() == rt.API_VERSION == 3
+    assert L.rt_api_version() == rt.API_VERSION == 4
 
 
 def golden_scene():
