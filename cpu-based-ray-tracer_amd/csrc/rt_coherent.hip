@@ -267,6 +267,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #endif
 // (the same for the direct term's two divisions in the BVH variant: C5 +0.1 %, within the spread --
 // profiles/r05/ab/ab_c5_nf_planes.json -- not kept)
+// the BVH variant's rounds walk a lane's two rays TOGETHER when both are pending (round 6): ray B rides in a
+// second walk slot of the near-first walk, its node load issued with ray A's, so a lane has two independent
+// node loads in flight instead of one (the walk waits on dependent loads: SQ_WAIT_ANY 45 %, profiles/r05/c5)
+#ifndef RT_BVH_PAIR
+#define RT_BVH_PAIR 0
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -1311,6 +1317,12 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     // compact walks end at the subtree's end, as the near-first orderings do (their exit reads NN)
                     const uint32_t tend = (kargs4().split_root != 0u && kargs4().force_walk == 0u && finite3(r.rcp)) ? kargs4().split_end : NN;
                     int parked0 = -1, parked1 = -1;
+#if RT_BVH_PAIR
+                    // ray B walks in a second slot when the lane's ray A is still walking too (the baked walk only)
+                    const bool pair = curA && tiB < NN && !occB && finite3(rcp3(dB));
+                    uint32_t ti2 = pair ? tiB : NN;
+                    int park2 = -1;
+#endif
                     auto walk_q = [&]() {
                         // every node's quantized box (16 B): an internal hit descends, a leaf hit parks the
                         // triangle; its exact box is tested with its vertices at the end of the round
@@ -1353,6 +1365,31 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                         // (two nodes per dependent load -- node ti and its pre-order successor, visited next when ti is
                         // entered or a leaf -- measured C5 -8 % at 7 waves (18 VGPRs spill) and -5 % at 6:
                         // profiles/r05/ab/ab_c5_walk_pair.json)
+#if RT_BVH_PAIR
+                        if (BAKED && pair) {
+                            // ray B in the second slot: both slots' node loads before either test; slot 2 parks one
+                            // leaf and stops stepping for the round
+                            const float4* wn2 = Q.wcopies + ((uint32_t)(dB.x < 0.0f) | ((uint32_t)(dB.y < 0.0f) << 1) | ((uint32_t)(dB.z < 0.0f) << 2)) * Q.wcopy_stride;
+                            const V3 rc2 = rcp3(dB);
+                            const float bound2 = slen * 1.00001f + 1e-5f;
+                            bool go1 = true;
+                            for (uint32_t s = 0; s < steps; ++s) {
+                                const bool g1 = go1 && ti < tend, g2 = ti2 < tend && park2 < 0;
+                                if (!(g1 || g2)) break;
+                                const uint32_t k1 = 2u * (g1 ? ti : 0u), k2 = 2u * (g2 ? ti2 : 0u);
+                                const float4 q0 = wn[k1], q1 = wn[k1 + 1], u0 = wn2[k2], u1 = wn2[k2 + 1];
+                                if (g1 && !test_node(q0, q1)) go1 = false;
+                                if (g2) {
+                                    const Ray r2{o, dB, rc2, dB.x < 0.0f, dB.y < 0.0f, dB.z < 0.0f};
+                                    const bool hit = slab_nf_within(r2, u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, bound2);
+                                    const int tri = f2i(u1.w);
+                                    ti2 = (hit && tri < 0) ? ti2 + 1 : (uint32_t)f2i(u1.z);
+                                    if (hit && tri >= 0) park2 = tri;
+                                }
+                            }
+                            return;
+                        }
+#endif
                         for (uint32_t s = 0; s < steps && ti < tend; ++s) {
                             const float4 q0 = wn[2 * ti];
                             const float4 q1 = wn[2 * ti + 1];
@@ -1405,6 +1442,21 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     if (ti >= tend) ti = NN;
                     if (curA) tiA = ti;
                     else tiB = ti;
+#if RT_BVH_PAIR
+                    if (pair) {
+                        // ray B's parked leaf: the shadow verdict (MC/Renderer.cpp:184)
+                        if (park2 >= 0) {
+                            const float4 t0 = S.tris[4 * park2], t1 = S.tris[4 * park2 + 1], t2 = S.tris[4 * park2 + 2];
+                            double t;
+                            if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, dB, t) &&
+                                !((double)slen < t + (double)0.01f)) {
+                                occB = true;
+                                ti2 = NN;
+                            }
+                        }
+                        tiB = ti2 >= tend ? NN : ti2;
+                    }
+#endif
                     SEC_MARK(5);
                 }
             }

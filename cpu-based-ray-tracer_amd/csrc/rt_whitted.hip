@@ -110,6 +110,87 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
     else walk(FiniteSlab{}, std::false_type{});
 }
 
+// The two lights' shadow rays of one hit walked TOGETHER (round 6): both start at the shading point, so the
+// lane carries two small walk states -- node index, reciprocal direction, bound, ordering base -- and every
+// step issues both rays' node loads before either test: two independent loads in flight per lane where the
+// sequential walks had one (the walk waits on L2 latency, not on issue: VALU issue 27 %, SQ_WAIT_ANY 61 %,
+// profiles/r05/c3).  A ray that meets a leaf parks it and stops stepping for the round; the round ends with
+// each ray's parked leaf tested.  The verdict is any hit with t * t < d2 (BV/Renderer.cpp:195): an existence
+// test, so the order of the walks does not matter, and boxes entered beyond the light are skipped with the same
+// margin as whitted_traverse.  Rays with a finite reciprocal direction and a scene with near-first orderings
+// only (the caller decides per wave).
+#ifndef RT_WH_PAIR
+#define RT_WH_PAIR 0
+#endif
+#ifndef RT_WH_PAIR_STEPS
+#define RT_WH_PAIR_STEPS 8
+#endif
+template <bool COUNT>
+__device__ __forceinline__ void whitted_shadow_pair(const KParams& P, const V3& x, const V3& sp, bool& occA, bool& occB, uint32_t& node_tests,
+                                                    uint32_t& tri_tests)
+{
+    const uint32_t n = P.n_nodes;
+    const float4* __restrict__ wo = P.worders;
+    const float4* __restrict__ tris = P.tris;
+    // light l's direction from x, normalized, and its squared distance: recomputed where needed (the same
+    // operations give the same bits), so the walk keeps no direction live -- only the reciprocals
+    auto light_dir = [&](uint32_t l, float& d2) {
+        const float4 lp = P.plights[2 * l];
+        const V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
+        d2 = dot(ld, ld);
+        return w_normalize(ld);
+    };
+    float d2a, d2b;
+    const V3 la = light_dir(0, d2a), lb = light_dir(1, d2b);
+    const V3 ra = V3{rcp_f32(la.x), rcp_f32(la.y), rcp_f32(la.z)}, rb = V3{rcp_f32(lb.x), rcp_f32(lb.y), rcp_f32(lb.z)};
+    const uint32_t oct = ((uint32_t)(la.x < 0.0f) | ((uint32_t)(la.y < 0.0f) << 1) | ((uint32_t)(la.z < 0.0f) << 2)) |
+                         (((uint32_t)(lb.x < 0.0f) | ((uint32_t)(lb.y < 0.0f) << 1) | ((uint32_t)(lb.z < 0.0f) << 2)) << 3);
+    const float bA = __builtin_sqrtf(d2a) * 1.00001f + 1e-5f, bB = __builtin_sqrtf(d2b) * 1.00001f + 1e-5f;
+    uint32_t ia = 0, ib = 0;
+    occA = occB = false;
+    auto shadow_test = [&](uint32_t l, int tri) -> bool {
+        if (COUNT) ++tri_tests;
+        float d2;
+        const V3 d = light_dir(l, d2);
+        const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
+        double t;
+        return moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, sp, d, t) && t * t < (double)d2;
+    };
+    auto slab = [&](const V3& rc, const float4& q0, const float4& q1, float bound) {   // slab_nf_within from sp
+        const float tix = (q0.x - sp.x) * rc.x, tiy = (q0.y - sp.y) * rc.y, tiz = (q0.z - sp.z) * rc.z;
+        const float tox = (q0.w - sp.x) * rc.x, toy = (q1.x - sp.y) * rc.y, toz = (q1.y - sp.z) * rc.z;
+        const float tin = __builtin_fmaxf(tix, __builtin_fmaxf(tiy, tiz));
+        const float tout = __builtin_fminf(tox, __builtin_fminf(toy, toz));
+        return (tout >= 0.0f) && (tin <= tout) && (tin <= bound);
+    };
+    while (ia < n || ib < n) {
+        int pa = -1, pb = -1;
+        for (uint32_t s = 0; s < RT_WH_PAIR_STEPS; ++s) {
+            const bool ga = ia < n && pa < 0, gb = ib < n && pb < 0;
+            if (!(ga || gb)) break;
+            // both node loads first (a finished ray reads node 0 of its ordering, discarded)
+            const uint32_t ka = 2u * n * (oct & 7u) + 2u * (ga ? ia : 0u), kb = 2u * n * (oct >> 3) + 2u * (gb ? ib : 0u);
+            const float4 a0 = wo[ka], a1 = wo[ka + 1], b0 = wo[kb], b1 = wo[kb + 1];
+            if (ga) {
+                if (COUNT) ++node_tests;
+                const bool hit = slab(ra, a0, a1, bA);
+                const int tri = f2i(a1.w);
+                ia = (hit && tri < 0) ? ia + 1 : (uint32_t)f2i(a1.z);
+                if (hit && tri >= 0) pa = tri;
+            }
+            if (gb) {
+                if (COUNT) ++node_tests;
+                const bool hit = slab(rb, b0, b1, bB);
+                const int tri = f2i(b1.w);
+                ib = (hit && tri < 0) ? ib + 1 : (uint32_t)f2i(b1.z);
+                if (hit && tri >= 0) pb = tri;
+            }
+        }
+        if (pa >= 0 && shadow_test(0, pa)) { occA = true; ia = n; }
+        if (pb >= 0 && shadow_test(1, pb)) { occB = true; ib = n; }
+    }
+}
+
 }  // namespace
 
 // frame groups per block: an 8x8 tile per block, wave g rendering the frames k = g (mod 4) of it; the
@@ -154,10 +235,35 @@ __device__ __forceinline__ V3 whitted_sample(const KParams& P, uint32_t lx, uint
         const V3 off = muls(n, INTERSECTION_CORRECTION);
         const V3 sp = (dot(ray.d, n) < 0.0f) ? add(x, off) : sub(x, off);
         V3 diffuse{0.0f, 0.0f, 0.0f};
-        // (the two lights' shadow rays walked together -- both rays' node loads issued before either test --
-        // measured 2-7 % slower at 6-8 waves per SIMD: 4-32 VGPRs spill; 7 waves alone -1.4 %,
-        // profiles/r05/ab/ab_c3_shadow2_waves.json)
-        for (uint32_t l = 0; l < P.n_plights; ++l) {
+        uint32_t l = 0;
+        if (RT_WH_PAIR && P.n_plights >= 2 && P.worders != nullptr) {
+            // lights 0 and 1: their shadow rays walked together when every lane's pair has finite reciprocals
+            // (wave-uniform: whitted_shadow_pair walks the near-first orderings only)
+            auto ldir = [&](uint32_t k) {
+                const float4 lp = P.plights[2 * k];
+                return w_normalize(sub(V3{lp.x, lp.y, lp.z}, x));
+            };
+            const V3 l0 = ldir(0), l1 = ldir(1);
+            const bool fin = rcp_finite(make_ray(sp, l0)) && rcp_finite(make_ray(sp, l1));
+            if (__all(fin)) {
+                // |dot(l, n)| of both lights now: the normal is not live across the walk
+                const float c0 = __builtin_fabsf(dot(l0, n)), c1 = __builtin_fabsf(dot(l1, n));
+                if (COUNT) rays += 2;
+                bool o0, o1;
+                whitted_shadow_pair<COUNT>(P, x, sp, o0, o1, node_tests, tri_tests);
+                // the diffuse sum in light order (BV/Renderer.cpp:186-199)
+                if (!o0) {
+                    const float4 lr4 = P.plights[1];
+                    diffuse = add(diffuse, V3{lr4.x * c0, lr4.y * c0, lr4.z * c0});
+                }
+                if (!o1) {
+                    const float4 lr4 = P.plights[3];
+                    diffuse = add(diffuse, V3{lr4.x * c1, lr4.y * c1, lr4.z * c1});
+                }
+                l = 2;
+            }
+        }
+        for (; l < P.n_plights; ++l) {
             const float4 lp = P.plights[2 * l], lr4 = P.plights[2 * l + 1];
             V3 ld = sub(V3{lp.x, lp.y, lp.z}, x);
             const float d2 = dot(ld, ld);
@@ -187,8 +293,11 @@ __device__ __forceinline__ void whitted_store(const KParams& P, uint32_t local, 
     P.rgba[local] = (to_u8(aw) << 24) | (to_u8(bz) << 16) | (to_u8(gy) << 8) | to_u8(rx);
 }
 
+#ifndef RT_WH_WAVES
+#define RT_WH_WAVES 8   // waves per SIMD the register budget is sized for
+#endif
 template <bool COUNT>
-__global__ void __launch_bounds__(256, 8) whitted_kernel(KParams P)
+__global__ void __launch_bounds__(256, RT_WH_WAVES) whitted_kernel(KParams P)
 {
     uint32_t node_tests = 0, tri_tests = 0, rays = 0;
     constexpr uint32_t FG = WH_FG;
