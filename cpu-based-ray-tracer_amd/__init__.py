@@ -60,7 +60,8 @@ class GroupStats(C.Structure):
     _fields_ = [("last_ms", C.c_float), ("max_member_kernel_ms", C.c_float), ("gather", C.c_uint32), ("n", C.c_uint32)]
 
 
-_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders", "rt_scene_whitted_orders"}   # may be absent from an older A/B build
+_DIAGNOSTIC = {"rt_debug_counters", "rt_read_accumulation", "rt_scene_walk_orders", "rt_scene_whitted_orders",
+               "rt_scene_whitted_orders_half"}   # may be absent from an older A/B build
 
 KERNEL_NAMES = {0: "pt_megakernel", 1: "pt_coherent_kernel", 2: "whitted_kernel", 3: "pt_coherent_kernel"}
 # rt_stats.kernel_reason (include/rt_capi.h RT_KERNEL_REASON_*)
@@ -131,6 +132,7 @@ def lib():
         "rt_scene_lbvh_host": (i32, [vp, fp, fp]),
         "rt_scene_walk_orders": (i32, [vp, fp, C.POINTER(C.c_uint64)]),
         "rt_scene_whitted_orders": (i32, [vp, fp, C.POINTER(C.c_uint64)]),
+        "rt_scene_whitted_orders_half": (i32, [vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
         "rt_debug_scene_arrays": (i32, [vp, fp, u32, fp, u32]),
         "rt_resize": (i32, [vp, u32, u32, u32, u32, u32]),
         "rt_local_rows": (u32, [vp]),
@@ -326,6 +328,18 @@ class Scene:
         out = np.zeros(n.value, np.float32)
         self._check(fn(self.h, _fp(out), C.byref(n)), name)
         return out.reshape(8, -1, 8)
+
+    def whitted_orders_half(self):
+        """The Whitted orderings in 16-byte half-plane nodes (rt_scene_whitted_orders_half): (8, n_nodes, 4) uint32,
+        or None."""
+        n = C.c_uint64(0)
+        self._check(lib().rt_scene_whitted_orders_half(self.h, None, C.byref(n)), "rt_scene_whitted_orders_half")
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, np.uint32)
+        self._check(lib().rt_scene_whitted_orders_half(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(n)),
+                    "rt_scene_whitted_orders_half")
+        return out.reshape(8, -1, 4)
 
     def export(self):
         i = self.info()

@@ -40,6 +40,7 @@ struct rt_ctx {
     int32_t* d_stri = nullptr;    // split trace: outside slot -> triangle
     float4* d_wcopies = nullptr;  // split trace: near-first orderings of the walked subtree (FlatScene::wcopies)
     float4* d_worders = nullptr;  // Whitted scenes: near-first orderings of the whole tree (FlatScene::worders)
+    uint4* d_worders_h = nullptr; // the same in 16-byte nodes, half planes rounded outward (FlatScene::worders_h)
     uint32_t split_root = 0, split_end = 0, n_sboxes = 0, n_sleaves = 0;
     uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
     float4 *d_tabc = nullptr, *d_tnrm = nullptr;
@@ -122,6 +123,7 @@ struct rt_ctx {
     bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
     bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
     bool wh_order = true;     // Whitted kernel: walk the whole tree's near-first ordering of the ray's octant (RT_WH_ORDER=0: DFS)
+    bool wh_half = true;      // ... in its 16-byte half-plane nodes (RT_WH_HALF=0: the 32-byte float nodes)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     uint32_t seg_min_parts = 128; // A/B (RT_SEG_MIN_PARTS): path-kernel parts per wave the split aims for
     uint32_t seg_part_lf = 4;     // A/B (RT_SEG_PART_LF): log2 of the fewest frames' worth of records in a part
@@ -460,6 +462,15 @@ rt_status rt_scene_whitted_orders(const rt_scene* s, float* out, uint64_t* n_flo
     return RT_OK;
 }
 
+rt_status rt_scene_whitted_orders_half(const rt_scene* s, uint32_t* out, uint64_t* n_words)
+{
+    if (!s || !s->built) return RT_ERR_STATE;
+    if (!n_words) return RT_ERR_INVALID;
+    *n_words = s->flat.worders_h.size();
+    if (out && !s->flat.worders_h.empty()) std::memcpy(out, s->flat.worders_h.data(), s->flat.worders_h.size() * sizeof(uint32_t));
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ context
 rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
 {
@@ -478,6 +489,7 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_SPLIT")) c->split = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WALK_ORDER")) c->walk_order = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_WH_ORDER")) c->wh_order = std::strtoul(e, nullptr, 10) != 0;
+    if (const char* e = rt_knob("RT_WH_HALF")) c->wh_half = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SEG_PARTS_OFF")) c->seg_parts_off = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_SEG_MIN_PARTS")) c->seg_min_parts = (uint32_t)std::max(1ul, std::strtoul(e, nullptr, 10));
     if (const char* e = rt_knob("RT_SEG_PART_LF")) c->seg_part_lf = (uint32_t)std::min(6ul, std::strtoul(e, nullptr, 10));
@@ -591,6 +603,9 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
         if ((r = upload(c, c->d_wcopies, walks ? s->flat.wcopies : kNone)) != RT_OK) return r;
         // (8 x the whole tree's nodes for a Whitted scene: 5.8 MB at C3)
         if ((r = upload(c, c->d_worders, c->wh_order ? s->flat.worders : kNone)) != RT_OK) return r;
+        // (half of that in 16-byte nodes, when the Whitted walk takes them: 2.9 MB at C3)
+        static const std::vector<uint32_t> kNoneU;
+        if ((r = upload(c, c->d_worders_h, c->wh_order && c->wh_half ? s->flat.worders_h : kNoneU)) != RT_OK) return r;
     }
     c->split_root = s->flat.split_root;
     c->split_end = s->flat.split_end;
@@ -676,7 +691,7 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     c->d_nodes = d_nodes; c->d_tris = d_tris;
     // the BVH-walking kernels: no leaf-box table, no compact tree
     dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
-    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders);   // the split and orderings refer to the host tree's node order
+    dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders); dfree(c->d_worders_h);   // the split and orderings refer to the host tree's node order
     c->split_root = c->split_end = c->n_sboxes = c->n_sleaves = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
@@ -766,6 +781,7 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
         }
     }
     P.worders = c->d_worders;
+    P.worders_h = (c->d_worders && c->d_worders_h && c->hdr.has_qnodes && c->d_tabc) ? c->d_worders_h : nullptr;
     P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
     P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;
     std::memcpy(P.q_origin, c->hdr.q_origin, sizeof P.q_origin);

@@ -25,6 +25,9 @@ struct KParams {
     // Whitted scenes: the whole tree's near-first orderings (FlatScene::worders; null: the DFS walk), ordering
     // o's node k at worders[2 * (o * n_nodes + k)]
     const float4* worders;
+    // the same orderings in 16-byte nodes with half planes rounded outward (FlatScene::worders_h; null: off), ordering
+    // o's node k at worders_h[o * n_nodes + k]; a leaf's exact box comes from its vertices (tabc)
+    const uint4* worders_h;
     // (the BVH variant stages the small tables (mats | lnodes | ltris) in LDS, the split's outside triangles
     //  (3 float4 per slot: a, e1, (e2, bits(triangle))) after them; rt_capi.cpp checks that they fit)
     // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex

@@ -165,6 +165,57 @@ int build_sah(std::vector<SNode>& nodes, std::vector<std::pair<Box, int>>& leave
     return me;
 }
 
+// IEEE half of a float rounded toward -inf (down) or +inf (up): the nearest half, stepped one half-ulp when it
+// lies on the wrong side (+-65504 beyond the half range round to +-inf on the outward side)
+uint16_t half_directed(float v, bool up)
+{
+    _Float16 h = (_Float16)v;
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    const float back = (float)h;
+    if (up ? back >= v : back <= v) return b;
+    // one step toward the requested side
+    const bool neg = (b & 0x8000u) != 0u;
+    const uint16_t mag = b & 0x7FFFu;
+    if (up) {
+        if (neg) return mag == 0u ? (uint16_t)0x0001u : (uint16_t)(b - 1u);   // -0 -> +min subnormal
+        return (uint16_t)(b + 1u);
+    }
+    if (!neg) return mag == 0u ? (uint16_t)0x8001u : (uint16_t)(b - 1u);
+    return (uint16_t)(b + 1u);
+}
+
+// 16-byte nodes of near-first orderings (FlatScene::worders_h): false when a leaf's successor is not the next
+// node of its ordering or an index does not fit
+bool compact_orderings(const std::vector<float>& src, uint32_t M, uint32_t first, std::vector<uint32_t>& dst)
+{
+    dst.assign((size_t)8 * M * 4, 0u);
+    for (uint32_t oct = 0; oct < 8; ++oct) {
+        const bool neg[3] = {(oct & 1u) != 0u, (oct & 2u) != 0u, (oct & 4u) != 0u};
+        for (uint32_t k = 0; k < M; ++k) {
+            const float* q = &src[((size_t)oct * M + k) * 8];
+            uint32_t* w = &dst[((size_t)oct * M + k) * 4];
+            for (int a = 0; a < 3; ++a) {
+                // near = the low plane unless the direction is negative on this axis (rt_scene.cpp near_first);
+                // a low plane rounds down, a high plane up
+                const uint16_t nh = half_directed(q[a], neg[a]), fh = half_directed(q[3 + a], !neg[a]);
+                w[a] = (uint32_t)nh | ((uint32_t)fh << 16);
+            }
+            int32_t skip, tri;
+            std::memcpy(&skip, &q[6], 4);
+            std::memcpy(&tri, &q[7], 4);
+            if (tri >= 0) {
+                if ((uint32_t)skip != first + k + 1u && !(k + 1u == M)) return false;
+                w[3] = 0x80000000u | (uint32_t)tri;
+            } else {
+                if (skip < 0) return false;
+                w[3] = (uint32_t)skip;
+            }
+        }
+    }
+    return true;
+}
+
 int build_bvh(std::vector<BNode>& nodes, std::vector<Item>& items, size_t lo, size_t hi)
 {
     const size_t n = hi - lo;
@@ -841,6 +892,9 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
             out.qnodes.clear();
         }
     }
+    // ---- the Whitted orderings in 16 bytes per node, where the exact leaf test has the vertices (tabc)
+    out.worders_h.clear();
+    if (!out.worders.empty() && out.hdr.has_qnodes && !compact_orderings(out.worders, NN, 0u, out.worders_h)) out.worders_h.clear();
     // ---- materials (one per mesh): brdf = diffuse_coefficient / PI, emitting = length(emission) > 1e-5
     const float PI = 3.141592653589793f;   // MC/WhittedUtilities.h:20
     out.mats.resize(nm * 8);

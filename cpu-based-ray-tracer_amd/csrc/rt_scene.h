@@ -67,6 +67,12 @@ struct FlatScene {
     // Whitted scenes (point lights): the whole tree in 8 near-first pre-orders, node k of ordering o at
     // [(o * n_nodes + k) * 8] (empty: the kernel walks `nodes`)
     std::vector<float> worders;
+    // the same orderings in 16 bytes per node (round 6): each plane as an IEEE half rounded OUTWARD (a low plane
+    // down, a high plane up: the decoded box contains the exact one), (near.x | far.x << 16, near.y | far.y << 16,
+    // near.z | far.z << 16, skip | internal, or 0x80000000 | triangle for a leaf, whose successor is the next
+    // node); built when every leaf's box is its triangle's vertex box (`tabc` holds the vertices for the exact
+    // leaf test); empty otherwise
+    std::vector<uint32_t> worders_h;
     std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
     std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag

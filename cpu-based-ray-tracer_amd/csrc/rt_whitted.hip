@@ -34,6 +34,9 @@ namespace {
 #ifndef RT_WH_STEPS
 #define RT_WH_STEPS 8
 #endif
+#ifndef RT_WH_HALF
+#define RT_WH_HALF 1   // walk the 16-byte half-plane orderings when the scene has them (P.worders_h)
+#endif
 
 
 struct FiniteSlab { static constexpr bool value = true; };
@@ -55,11 +58,10 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
     const float4* __restrict__ tris = P.tris;
     const uint32_t n = P.n_nodes;
     const float sbound = shadow ? __builtin_sqrtf((float)d2) * 1.00001f + 1e-5f : 0.0f;
-    auto tri_test = [&](int tri) -> bool {   // true: the shadow ray is occluded (the walk ends)
+    auto tri_test_v = [&](int tri, const V3& va, const V3& e1, const V3& e2) -> bool {   // true: the shadow ray is occluded
         if (COUNT) ++tri_tests;
-        const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
         double t;
-        if (moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t)) {
+        if (moller_trumbore(va, e1, e2, r, t)) {
             if (shadow) {
                 // (shadow_record.has_intersection) && (t * t < light_distance_squared), BV/Renderer.cpp:195
                 if (t * t < d2) { occluded = true; return true; }
@@ -70,6 +72,51 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
             }
         }
         return false;
+    };
+    auto tri_test = [&](int tri) -> bool {
+        const float4 t0 = tris[4 * tri], t1 = tris[4 * tri + 1], t2 = tris[4 * tri + 2];
+        return tri_test_v(tri, V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z});
+    };
+    // the 16-byte orderings (P.worders_h, rt_scene.cpp compact_orderings): one 16-byte load per step instead of two,
+    // half planes rounded outward -- a decoded box contains the exact one, so for a finite ray the walk visits every
+    // box the exact walk visits (and maybe more), and a box entered beyond the bound is still beyond it -- and a
+    // leaf the half box passes is tested against its EXACT box, its triangle's vertex box (Triangle::Get3DAABB,
+    // BV/TriangleMesh.h; the same floats as the tree's leaf box, checked on the host), before Moller-Trumbore: the
+    // candidates are exactly the float walk's.  (C3's walk is bound by the vL1D's gather rate -- 1.35 node loads
+    // per CU-clock of the calibrated 1.54 in round 5 -- so the node bytes per step are the lever, not the latency.)
+    auto walk_half = [&]() {
+        const uint4* __restrict__ wh = P.worders_h + n * ((uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2));
+        const float4* __restrict__ tabc = P.tabc;
+        auto h2f = [](uint32_t b) { return (float)__builtin_bit_cast(_Float16, (unsigned short)b); };
+        uint32_t i = 0;
+        while (i < n) {
+            const float bound = shadow ? sbound : ((best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff());
+            int p0 = -1, p1 = -1;
+            for (uint32_t s = 0; s < RT_WH_STEPS && i < n; ++s) {
+                if (COUNT) ++node_tests;
+                const uint4 q = wh[i];
+                const bool hit = slab_nf_within(r, h2f(q.x & 0xFFFFu), h2f(q.y & 0xFFFFu), h2f(q.z & 0xFFFFu), h2f(q.x >> 16), h2f(q.y >> 16),
+                                                h2f(q.z >> 16), bound);
+                const bool leaf = (q.w & 0x80000000u) != 0u;
+                i = (hit || leaf) ? i + 1 : q.w;
+                if (hit && leaf) {
+                    const int tri = (int)(q.w & 0x7FFFFFFFu);
+                    if (p0 < 0) p0 = tri;
+                    else { p1 = tri; break; }
+                }
+            }
+            for (int k = 0; k < 2; ++k) {
+                const int tri = k == 0 ? p0 : p1;
+                if (tri < 0) continue;
+                const float4 a = tabc[3 * tri], b = tabc[3 * tri + 1], c = tabc[3 * tri + 2];
+                if (!slab_hit_finite_within(r, __builtin_fminf(__builtin_fminf(a.x, b.x), c.x), __builtin_fminf(__builtin_fminf(a.y, b.y), c.y),
+                                            __builtin_fminf(__builtin_fminf(a.z, b.z), c.z), __builtin_fmaxf(__builtin_fmaxf(a.x, b.x), c.x),
+                                            __builtin_fmaxf(__builtin_fmaxf(a.y, b.y), c.y), __builtin_fmaxf(__builtin_fmaxf(a.z, b.z), c.z), bound))
+                    continue;
+                const V3 va{a.x, a.y, a.z};
+                if (tri_test_v(tri, va, sub(V3{b.x, b.y, b.z}, va), sub(V3{c.x, c.y, c.z}, va))) return;
+            }
+        }
     };
     auto walk = [&](auto kind, auto baked) {
         constexpr bool FIN = decltype(kind)::value;
@@ -106,6 +153,7 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
         }
     };
     if (!rcp_finite(r)) walk(GeneralSlab{}, std::false_type{});
+    else if (RT_WH_HALF && P.worders_h != nullptr) walk_half();
     else if (P.worders != nullptr) walk(FiniteSlab{}, std::true_type{});
     else walk(FiniteSlab{}, std::false_type{});
 }

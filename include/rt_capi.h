@@ -143,6 +143,10 @@ rt_status rt_scene_walk_orders(const rt_scene* s, float* out, uint64_t* n_floats
  * nodes in the same layout (a skip pointer past the last node reads n_nodes; 0 floats: none).  The Whitted
  * kernel walks the ordering of a finite ray's octant (knob RT_WH_ORDER=0: the DFS order). */
 rt_status rt_scene_whitted_orders(const rt_scene* s, float* out, uint64_t* n_floats);
+/* The same orderings in the Whitted kernel's 16-byte nodes (round 6), for tests: 8 x n_nodes x 4 words -- (near.x |
+ * far.x << 16, near.y | far.y << 16, near.z | far.z << 16, skip or 0x80000000 | triangle), each plane an IEEE half
+ * rounded outward; *n_words receives the size (0: none). */
+rt_status rt_scene_whitted_orders_half(const rt_scene* s, uint32_t* out, uint64_t* n_words);
 
 /* ------------------------------------------------------------------ camera (host math) */
 typedef struct {

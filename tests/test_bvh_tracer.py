@@ -125,6 +125,24 @@ def test_c3_full_image_digest(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("half", ["1", "0"], ids=["half-nodes", "float-nodes"])
+def test_c3_full_image_node_formats(scene, monkeypatch, half):
+    """The walk's 16-byte half-plane orderings (round 6, rt_whitted.hip walk_half: outward-rounded boxes, exact leaf
+    boxes from the vertices) and the 32-byte float orderings (RT_WH_HALF=0) give the reference's C3 frame bit for
+    bit, on the product (non-counting) kernel."""
+    z = np.load(os.path.join(G, "bvh_images.npz"))
+    monkeypatch.setenv("RT_WH_HALF", half)
+    c = rt.Context(0)
+    try:
+        c.upload(scene)
+        rgba, acc = render(c, 1280, 960, 64)
+    finally:
+        c.close()
+    assert hashlib.sha256(np.ascontiguousarray(acc).tobytes()).hexdigest() == str(z["sha_accum_1280x960_spp64"])
+    assert hashlib.sha256(np.ascontiguousarray(rgba).tobytes()).hexdigest() == str(z["sha_rgba_1280x960_spp64"])
+
+
+@pytest.mark.gpu
 def test_incremental_and_row_bands(ctx):
     """Render(+1 spp) x3 == one 3-spp launch; a 3-rank band split reassembles to the same bits."""
     z = np.load(os.path.join(G, "bvh_images.npz"))

@@ -154,6 +154,38 @@ def test_whitted_orders_of_c3(walk_tree, monkeypatch):
     check_orders(sc, n_rays=30, seed=3, same_tree=walk_tree == "0", whitted=True)
 
 
+def test_whitted_half_orders_contain_the_float_boxes():
+    """The Whitted kernel's 16-byte orderings (rt_scene.cpp compact_orderings): node for node the float orderings'
+    structure (skip of an internal node, triangle of a leaf, whose successor is the next node), and every half
+    plane rounded OUTWARD -- the near plane toward the ray's origin side and the far plane away, i.e. a low plane
+    down and a high plane up -- so the decoded box contains the exact box (the walk visits a superset; leaves are
+    then tested on their exact vertex boxes, rt_whitted.hip walk_half)."""
+    z = np.load(SA.A.__file__.replace("test_skip_adversarial.py", "golden/bvh_scene.npz"))
+    sc = rt.Scene.bvh_tracer(z["raw_bunny"], z["raw_teapot"])
+    fo = sc.walk_orders(whitted=True)
+    ho = sc.whitted_orders_half()
+    assert ho is not None and ho.shape[:2] == fo.shape[:2]
+    fi = np.ascontiguousarray(fo).view(np.int32)
+    skip, tri = fi[..., 6], fi[..., 7]
+    leaf = tri >= 0
+    w3 = ho[..., 3]
+    assert np.array_equal(w3[leaf] & 0x7FFFFFFF, tri[leaf].astype(np.uint32)) and np.all(w3[leaf] >> 31 == 1)
+    assert np.array_equal(w3[~leaf], skip[~leaf].astype(np.uint32))
+    k = np.arange(fo.shape[1])
+    assert np.all((skip == k[None, :] + 1)[leaf])   # a leaf's successor is the next node
+    half = lambda w: (w & 0xFFFF).astype(np.uint16).view(np.float16).astype(np.float32)
+    for a in range(3):
+        neg = ((np.arange(8) >> a) & 1).astype(bool)[:, None]
+        near_h, far_h = half(ho[..., a]), half(ho[..., a] >> 16)
+        near_f, far_f = fo[..., a], fo[..., 3 + a]
+        lo_ok = np.where(neg, far_h <= far_f, near_h <= near_f)    # the low plane rounded down
+        hi_ok = np.where(neg, near_h >= near_f, far_h >= far_f)    # the high plane rounded up
+        assert np.all(lo_ok) and np.all(hi_ok), a
+        # and by at most one half-ulp (the nearest half, stepped once when on the wrong side)
+        err = np.abs(near_h.astype(np.float64) - near_f) / np.maximum(np.abs(near_f.astype(np.float64)), 2.0 ** -14)
+        assert float(err.max()) <= 2.0 ** -10
+
+
 @pytest.mark.parametrize("bins", ["2", "1024"])
 def test_sah_bins_build_other_trees(bins, monkeypatch):
     """RT_SAH_BINS (the A/B knob of the SAH build's bins per axis) builds another tree over the same leaves: its
