@@ -123,7 +123,7 @@ struct rt_ctx {
     bool split = true;   // larger scenes: the split trace when the scene has one (RT_SPLIT=0 disables)
     bool walk_order = true;   // split trace: walk the subtree's near-first ordering of the ray's octant (RT_WALK_ORDER=0: DFS)
     bool wh_order = true;     // Whitted kernel: walk the whole tree's near-first ordering of the ray's octant (RT_WH_ORDER=0: DFS)
-    bool wh_half = true;      // ... in its 16-byte half-plane nodes (RT_WH_HALF=0: the 32-byte float nodes)
+    bool wh_half = false;     // ... in its 16-byte half-plane nodes (RT_WH_HALF=1 with a -DRT_WH_HALF=1 build: an A/B)
     bool seg_parts_off = false;   // A/B (RT_SEG_PARTS_OFF=1): short pre-pass segments, one path-kernel part each
     uint32_t seg_min_parts = 128; // A/B (RT_SEG_MIN_PARTS): path-kernel parts per wave the split aims for
     uint32_t seg_part_lf = 4;     // A/B (RT_SEG_PART_LF): log2 of the fewest frames' worth of records in a part

@@ -127,9 +127,10 @@ def test_c3_full_image_digest(ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("half", ["1", "0"], ids=["half-nodes", "float-nodes"])
 def test_c3_full_image_node_formats(scene, monkeypatch, half):
-    """The walk's 16-byte half-plane orderings (round 6, rt_whitted.hip walk_half: outward-rounded boxes, exact leaf
-    boxes from the vertices) and the 32-byte float orderings (RT_WH_HALF=0) give the reference's C3 frame bit for
-    bit, on the product (non-counting) kernel."""
+    """The 32-byte float orderings (the product) and, with RT_WH_HALF=1, the upload of the 16-byte half-plane
+    orderings (round 6, rt_whitted.hip walk_half: outward-rounded boxes, exact leaf boxes from the vertices; walked by
+    a -DRT_WH_HALF=1 build, an A/B measured -3 %) give the reference's C3 frame bit for bit on the product
+    (non-counting) kernel."""
     z = np.load(os.path.join(G, "bvh_images.npz"))
     monkeypatch.setenv("RT_WH_HALF", half)
     c = rt.Context(0)
