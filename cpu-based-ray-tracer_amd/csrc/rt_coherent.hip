@@ -273,6 +273,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_BVH_PAIR
 #define RT_BVH_PAIR 0
 #endif
+// the walk fallback (a non-finite reciprocal direction) and the pre-pass's walk without the sphere branch: these kernels
+// never see a sphere (rt_capi.cpp: scenes with spheres render on the megakernel); 1 keeps it (4 spilled VGPRs in the
+// leaf-box path kernel, 78 instead of 73 in the pre-pass: DESIGN.md 5.1)
+#ifndef RT_COH_SPH
+#define RT_COH_SPH 0
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -1090,13 +1096,13 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 const Ray r{o, dA, rA, dA.x < 0.0f, dA.y < 0.0f, dA.z < 0.0f};
                 bool dummy = false;
                 tA = 1.7976931348623157e308;
-                traverse_impl<false, false>(S, r, false, 0.0, tA, triA, dummy, nt, tt);
+                traverse_impl<false, false, RT_COH_SPH>(S, r, false, 0.0, tA, triA, dummy, nt, tt);
             }
             if (trB) {
                 const Ray r{o, dB, rB, dB.x < 0.0f, dB.y < 0.0f, dB.z < 0.0f};
                 double db = 1.7976931348623157e308;
                 int dt = -1;
-                traverse_impl<false, false>(S, r, true, (double)slen, db, dt, occB, nt, tt);
+                traverse_impl<false, false, RT_COH_SPH>(S, r, true, (double)slen, db, dt, occB, nt, tt);
             }
         }
         SEC_MARK(6);
@@ -1771,8 +1777,8 @@ __global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
             // (the reference's traversal, rt_path.h)
             bool occ = false;
             uint32_t nt = 0, tt = 0;
-            if (fin) traverse_impl<false, true>(S, r, false, 0.0, t, tri, occ, nt, tt);
-            else traverse_impl<false, false>(S, r, false, 0.0, t, tri, occ, nt, tt);
+            if (fin) traverse_impl<false, true, RT_COH_SPH>(S, r, false, 0.0, t, tri, occ, nt, tt);
+            else traverse_impl<false, false, RT_COH_SPH>(S, r, false, 0.0, t, tri, occ, nt, tt);
         }
         bool surface = false;
         float4 rec = make_float4(0.f, 0.f, 0.f, 0.f);

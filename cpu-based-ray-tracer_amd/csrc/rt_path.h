@@ -63,11 +63,13 @@ struct SceneView {
 };
 
 // A leaf's primitive: Moller-Trumbore on a triangle slot, the sphere quadratic on a sphere slot (the flag in
-// q2.w, rt_layout.h; scenes with spheres render on the megakernel)
+// q2.w, rt_layout.h; scenes with spheres render on the megakernel).  SPH = false for the kernels that never see a
+// sphere (the vertex-synchronous kernel and its pre-pass): the sphere branch cost their walk fallback 4 spilled VGPRs
+template <bool SPH = true>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int slot, const Ray& r, double& t)
 {
     const float4 t0 = S.tris[4 * slot], t1 = S.tris[4 * slot + 1], t2 = S.tris[4 * slot + 2];
-    if (__float_as_uint(t2.w) != 0u) return sphere_hit(V3{t0.x, t0.y, t0.z}, t1.x, r, t);
+    if (SPH && __float_as_uint(t2.w) != 0u) return sphere_hit(V3{t0.x, t0.y, t0.z}, t1.x, r, t);
     return moller_trumbore(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, r, t);
 }
 // the surface normal of a hit at `loc`: a triangle's face normal (q3), a sphere's Whitted::normalize(loc - center)
@@ -89,7 +91,7 @@ __device__ __forceinline__ V3 leaf_normal(const SceneView& S, int slot, const V3
 // parked triangles are intersected together (Aila & Laine's while-while), so the Moller-Trumbore
 // body runs once per "leaf round" instead of once per box step.  Each lane still tests its
 // triangles in DFS order, so the tie rule (later leaf wins) and the any-hit exit are unchanged.
-template <bool COUNT, bool FINITE>
+template <bool COUNT, bool FINITE, bool SPH = true>
 __device__ __forceinline__ void traverse_impl(const SceneView& S, const Ray& r, bool shadow, double slen, double& best, int& best_tri,
                                               bool& occluded, uint32_t& node_tests, uint32_t& tri_tests)
 {
@@ -111,7 +113,7 @@ __device__ __forceinline__ void traverse_impl(const SceneView& S, const Ray& r, 
         if (parked >= 0) {
             if (COUNT) ++tri_tests;
             double t;
-            if (leaf_hit(S, parked, r, t)) {
+            if (leaf_hit<SPH>(S, parked, r, t)) {
                 if (shadow) {
                     // not occluded iff length(q-p) < t + 0.01f for every hit (MC/Renderer.cpp:184)
                     if (!(slen < t + (double)0.01f)) { occluded = true; i = n; }
