@@ -1,7 +1,8 @@
 """The vertex kernel's compile-time variants still build (CPU; hipcc cross-compiles for gfx950): the section
 timing diagnostics (RT_SECTIONS=1 and the candidate-histogram level 3, tools/prof_one.py) and the
-waves-per-SIMD settings measured in DESIGN.md 6.4, and the round-4 A/B switches (the drain without the pending
-fold, the BVH variant's division kind, the zero-numerator short division).  The product build is the Makefile's; these compile
+waves-per-SIMD settings measured in DESIGN.md 6.4, the round-4 A/B switches (the drain without the pending
+fold, the BVH variant's division kind, the zero-numerator short division) and the round-6 ones (the C5 A + B pair walk,
+the walk fallback with the sphere branch; in rt_whitted.hip the shadow-ray pair walk and the half-plane orderings).  The product build is the Makefile's; these compile
 rt_coherent.hip alone, device code only, so a diagnostic that is not built by default cannot rot."""
 import os
 import shutil
@@ -17,11 +18,15 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("flags", ["-DRT_SECTIONS=1", "-DRT_SECTIONS=3", "-DRT_COH_MIN_WAVES=7 -DRT_COH_BVH_MIN_WAVES=7",
                                    "-DRT_PEND_FOLD=0 -DRT_COH_BVH_PRE_MIN_WAVES=8",
-                                   "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0"])
+                                   "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0", "-DRT_BVH_PAIR=1 -DRT_COH_SPH=1",
+                                   "@rt_whitted.hip -DRT_WH_PAIR=1 -DRT_WH_WAVES=6", "@rt_whitted.hip -DRT_WH_HALF=1"])
 def test_coherent_kernel_variant_compiles(flags, tmp_path):
     cmd = [HIPCC, "-std=c++20", "-O3", "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), "-ffp-contract=off",
            "-fno-fast-math", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
            "-fno-slp-vectorize", "--cuda-device-only", "-c", os.path.join(PKG, "csrc", "rt_coherent.hip"), "-o", str(tmp_path / "k.o")]
-    cmd[1:1] = flags.split()
+    words = flags.split()
+    if words[0].startswith("@"):   # another kernel source
+        cmd[cmd.index(os.path.join(PKG, "csrc", "rt_coherent.hip"))] = os.path.join(PKG, "csrc", words.pop(0)[1:])
+    cmd[1:1] = words
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]

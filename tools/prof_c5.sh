@@ -1,13 +1,14 @@
 #!/bin/bash
 # tools/prof_c5.sh TAG [SPP] -- rocprofv3 kernel trace + PMC passes of the C5 render (3840x2160, the
 # vertex kernel's BVH variant) through tools/prof_one.py; each pass its own run (MI355X_MICROARCH.md).
+# PROF_LIB=librt_hip_x.so profiles an A/B build instead of the product library.
 set -euo pipefail
 TAG=${1:-c5}; SPP=${2:-64}
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$REPO/tools/prof_one.py librt_hip.so --scene c5 --width 3840 --height 2160 --spp $SPP"
+ARGS="$REPO/tools/prof_one.py ${PROF_LIB:-librt_hip.so} --scene c5 --width 3840 --height 2160 --spp $SPP"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- python3 $ARGS > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o pmc -- python3 $ARGS > "$OUT/pmc_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o pmc -- python3 $ARGS > "$OUT/pmc_write.log" 2>&1

@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/prof_scene.sh TAG PROF_ONE_ARGS... -- rocprofv3 kernel trace + PMC passes of one render shape through
 # tools/prof_one.py (e.g. --scene c3 --width 1280 --height 960 --spp 64); each pass its own run
-# (MI355X_MICROARCH.md), each under its own time limit; the first failure ends the script.
+# (MI355X_MICROARCH.md), each under its own time limit; the first failure ends the script.  PROF_LIB=librt_hip_x.so
+# profiles an A/B build instead of the product library.
 set -euo pipefail
 TAG=${1:?usage: prof_scene.sh TAG ARGS...}
 shift
@@ -9,7 +10,7 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$REPO/tools/prof_one.py librt_hip.so $*"
+ARGS="$REPO/tools/prof_one.py ${PROF_LIB:-librt_hip.so} $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace -- python3 $ARGS > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_sq" -o pmc -- python3 $ARGS > "$OUT/pmc_sq.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_tcc" -o pmc -- python3 $ARGS > "$OUT/pmc_tcc.log" 2>&1
