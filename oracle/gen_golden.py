@@ -17,6 +17,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py full       # C2 and C4 at their full spp (full_c2 / full_c4: one of them)
     python oracle/gen_golden.py full_c5    # C5 (Cornell + 79k-triangle bunny) at 3840x2160x256 (~10 min)
     python oracle/gen_golden.py full_c5_4096  # C5 at its full 4096 spp, every 64th row (~10 min)
+    python oracle/gen_golden.py full_c5_4096_mid  # the same frame's rows 32, 96, ... (round 6)
 """
 import os
 import subprocess
@@ -346,25 +347,26 @@ def c5_obj():
     return obj
 
 
-def gen_full_c5(spp=256, row_stride=1):
+def gen_full_c5(spp=256, row_stride=1, row_offset=0):
     """C5's launch shape: the Cornell box + the 79,488-triangle bunny at 3840x2160,
     seed 0, RR 0.8, frames 1..spp, through the reference's own TriangleMesh + BVH (MC/Renderer.cpp:114-133
     accumulation over all frames; MC/BVH.h:72-101 traversal).  2.1 G samples at 256 spp: long enough that
     some paths exceed the 624 words of one engine fill, so the harness re-fills the injected stream at the
     top of a shading call (mt_inject.h refill_if_near).  Stores the SHA-256 of the float4 accumulation and
-    of the RGBA8 frame, and every 64th row of the accumulation's rgb."""
+    of the RGBA8 frame, and every 64th row of the accumulation's rgb.  row_offset (round 6): the rows
+    y % 64 == row_offset instead, a second fixture of the same frame (full_c5_4096_mid: the rows halfway between)."""
     import hashlib
     import time
     W, H = 3840, 2160
     obj = c5_obj()
     t0 = time.time()
-    extra = [C5_FULL_ROW_STRIDE] if row_stride > 1 else []
+    extra = ([C5_FULL_ROW_STRIDE] + ([row_offset] if row_offset else [])) if row_stride > 1 else []
     run("image", CORNELL_DIR, obj, W, H, spp, 0, 0.8, os.cpu_count() or 8, tmp("acc"), tmp("rgba"), tmp("stats"), *extra)
     secs = time.time() - t0
     acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
     rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
-    rows = np.arange(0, H, C5_FULL_ROW_STRIDE)
-    name = "full_c5" if spp == 256 else f"full_c5_{spp}"
+    rows = np.arange(row_offset, H, C5_FULL_ROW_STRIDE)
+    name = ("full_c5" if spp == 256 else f"full_c5_{spp}") + ("_mid" if row_offset else "")
     # (rows only: the SHA-256 of the committed rows' accumulation and RGBA8 instead of the whole frame's)
     sel_acc, sel_rgba = (acc, rgba) if row_stride == 1 else (np.ascontiguousarray(acc[rows]), np.ascontiguousarray(rgba[rows]))
     np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), W=np.int64(W), H=np.int64(H), spp=np.int64(spp),
@@ -736,6 +738,8 @@ def main():
         if only == "full_c5_4096":
             # C5's full spp on every 64th row (the whole frame would take ~11 h on 8 cores): 535 M samples, ~10 min
             gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE)
+        if only == "full_c5_4096_mid":
+            gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=C5_FULL_ROW_STRIDE // 2)
     print("golden fixtures written to", GOLDEN)
 
 

@@ -441,10 +441,10 @@ static int cmd_camera(uint32_t W, uint32_t H, uint32_t frame, uint64_t seed, con
     return 0;
 }
 
-// (row_stride > 1: only the rows y % row_stride == 0 are rendered -- a full-spp fixture of selected rows; the others
-// stay zero)
+// (row_stride > 1: only the rows y % row_stride == row_offset are rendered -- a full-spp fixture of selected rows; the
+// others stay zero)
 static int cmd_image(const char* dir, const char* extra, uint32_t W, uint32_t H, uint32_t spp, uint64_t seed, float rr, int threads,
-                     const char* out_accum, const char* out_rgba, const char* out_stats, uint32_t row_stride = 1)
+                     const char* out_accum, const char* out_rgba, const char* out_stats, uint32_t row_stride = 1, uint32_t row_offset = 0)
 {
     Scene* s = build_cornell(dir, split_extra(extra));
     Camera cam{35.0f, 0.1f, 100.0f};
@@ -458,7 +458,7 @@ static int cmd_image(const char* dir, const char* extra, uint32_t W, uint32_t H,
         set_msvc_distribution();
         Counters local;
         for (;;) {
-            uint32_t y = next_row.fetch_add(1) * row_stride;
+            uint32_t y = next_row.fetch_add(1) * row_stride + row_offset;
             if (y >= H) break;
             for (uint32_t x = 0; x < W; ++x) {
                 uint32_t px = y * W + x;
@@ -606,9 +606,10 @@ int main(int argc, char** argv)
         return cmd_image_mt(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), (float)atof(argv[6]), argv[7]);
     if (c == "bench_mt" && argc == 9)
         return cmd_bench_mt(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), (float)atof(argv[7]), atoi(argv[8]));
-    if (c == "image" && (argc == 13 || argc == 14))
+    if (c == "image" && argc >= 13 && argc <= 15)
         return cmd_image(argv[2], argv[3], atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), strtoull(argv[7], 0, 10), (float)atof(argv[8]), atoi(argv[9]),
-                         argv[10], argv[11], argv[12], argc == 14 ? (uint32_t)std::max(1, atoi(argv[13])) : 1u);
+                         argv[10], argv[11], argv[12], argc >= 14 ? (uint32_t)std::max(1, atoi(argv[13])) : 1u,
+                         argc >= 15 ? (uint32_t)std::max(0, atoi(argv[14])) : 0u);
     fprintf(stderr, "bad command\n");
     return 1;
 }

@@ -85,7 +85,7 @@ def test_bench_rccl_branch_one_rank(tmp_path, W, H, spp):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"), "--gpus", "1", "--force-dist", "--dist-backend", "nccl",
            "--steps", "2", "--warmup", "1", "--width", str(W), "--height", str(H), "--spp", str(spp), "--no-cpu-baseline",
-           "--no-fast-probe", "--no-c5", "--dump-image", str(img)]
+           "--no-fast-probe", "--no-c5", "--no-small-configs", "--dump-image", str(img)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

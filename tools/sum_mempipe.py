@@ -32,7 +32,10 @@ def main():
     g = tot.get("GRBM_GUI_ACTIVE")
     out = {"kernel": args.kernel, "counters": tot}
     if g:
-        # GRBM_GUI_ACTIVE counts GPU clocks; TA_BUSY_avr is per TA instance (one per CU); the TD/TCP sums add all CUs
+        # GRBM_GUI_ACTIVE is reported summed over the 8 XCDs (profiles/summarize_pmc.py: XCDS), so the kernel's clocks
+        # are a eighth of it; TA_BUSY_avr is per TA instance (one per CU); the TD/TCP sums add all CUs
+        g = g / 8.0
+        out["kernel_clocks"] = g
         ncu = 256
         r = {}
         if "TA_BUSY_avr" in tot:
