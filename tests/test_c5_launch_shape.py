@@ -13,8 +13,9 @@ for paths longer than one engine fill (oracle/ref/mt_inject.h) -- via `oracle/ge
 the SHA-256 of the float4 accumulation and of the RGBA8 frame, and every 64th accumulation row.
 tests/golden/full_c5_4096.npz is the same at C5's full 4096 spp on every 64th row (`gen_golden.py full_c5_4096`:
 the harness renders only those rows -- the whole frame would take ~11 h on 8 cores); its SHA-256 covers those
-rows.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at the default budget) and
-compares the rows."""
+rows.  tests/golden/full_c5_4096_mid.npz (round 6) holds the rows halfway between (32, 96, ...), so the 4096-spp
+frame is pinned on every 32nd row.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
+the default budget) and compares the rows of both."""
 import hashlib
 import os
 
@@ -44,11 +45,13 @@ def scene(bunny_raw):
 
 def test_fixture_present_and_shaped():
     assert "full_c5" in FIXTURES
-    for name in FIXTURES:
+    for name in FIXTURES + ["full_c5_4096_mid"]:
+        if not os.path.exists(os.path.join(O.GOLDEN, f"{name}.npz")):
+            continue
         z = np.load(os.path.join(O.GOLDEN, f"{name}.npz"))
         W, H, spp = int(z["W"]), int(z["H"]), int(z["spp"])
         assert (W, H, int(z["seed"]), int(z["first_frame"])) == (3840, 2160, 0, 1) and spp in (256, 4096)
-        assert np.array_equal(z["rows"], np.arange(0, H, 64))
+        assert np.array_equal(z["rows"], np.arange(32 if name.endswith("_mid") else 0, H, 64))
         assert z["accum_rows"].shape == (len(z["rows"]), W, 3)
         assert np.all((z["rgba_rows"] >> 24) == 255)
         # samples; no harness overflow (every path read the injected stream, however long)
@@ -99,15 +102,19 @@ def test_c5_frame_in_launch_shape(scene, monkeypatch, name, budget_mb, min_passe
         assert st.last_prepass_ms > 0.0   # the split scene's camera pre-pass ran (in every pass)
     finally:
         c.close()
-    rows = acc[z["rows"], :, :3]
-    same = np.all(bits(rows) == bits(z["accum_rows"]), axis=-1)
-    assert same.all(), f"{same.mean():.6%} of the committed rows' pixels bitwise equal"
-    assert np.array_equal(rgba[z["rows"]], z["rgba_rows"])
-    rows_only = bool(z["rows_only"]) if "rows_only" in z.files else False
-    sel_acc = np.ascontiguousarray(acc[z["rows"]] if rows_only else acc)
-    sel_rgba = np.ascontiguousarray(rgba[z["rows"]] if rows_only else rgba)
-    assert hashlib.sha256(sel_acc.tobytes()).hexdigest() == str(z["sha_accum"])
-    assert hashlib.sha256(sel_rgba.tobytes()).hexdigest() == str(z["sha_rgba"])
+    zs = [z]
+    if name == "full_c5_4096" and os.path.exists(os.path.join(O.GOLDEN, "full_c5_4096_mid.npz")):
+        zs.append(np.load(os.path.join(O.GOLDEN, "full_c5_4096_mid.npz")))   # the same frame's rows 32, 96, ... (round 6)
+    for z in zs:
+        rows = acc[z["rows"], :, :3]
+        same = np.all(bits(rows) == bits(z["accum_rows"]), axis=-1)
+        assert same.all(), f"{same.mean():.6%} of the committed rows' pixels bitwise equal"
+        assert np.array_equal(rgba[z["rows"]], z["rgba_rows"])
+        rows_only = bool(z["rows_only"]) if "rows_only" in z.files else False
+        sel_acc = np.ascontiguousarray(acc[z["rows"]] if rows_only else acc)
+        sel_rgba = np.ascontiguousarray(rgba[z["rows"]] if rows_only else rgba)
+        assert hashlib.sha256(sel_acc.tobytes()).hexdigest() == str(z["sha_accum"])
+        assert hashlib.sha256(sel_rgba.tobytes()).hexdigest() == str(z["sha_rgba"])
 
 
 @pytest.mark.gpu
