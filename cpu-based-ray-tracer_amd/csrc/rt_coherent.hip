@@ -279,6 +279,13 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 #ifndef RT_COH_SPH
 #define RT_COH_SPH 0
 #endif
+// the leaf-box variant's Moller-Trumbore on packed pairs (rt_device.h moller_trumbore_pk: the same IEEE operations, 12
+// VALU fewer): C4 -3.3 %, bitwise (profiles/r06/ab/ab_c4_mt_packed.json) -- a v_pk_*_f32 of a wave64 occupies the
+// SIMD twice as long as the scalar instruction on gfx950, so packing buys no issue cycles, and the build spills 2
+// VGPRs; off (debug_primitives_kernel still checks the packed form against moller_trumbore_od bit for bit)
+#ifndef RT_MT_PK
+#define RT_MT_PK 0
+#endif
 constexpr int BOX_UNROLL = RT_BOX_UNROLL;
 constexpr uint32_t DRAIN_STEP = RT_DRAIN_STEP;
 constexpr uint32_t DRAIN_BATCH = RT_DRAIN_BATCH;
@@ -1159,7 +1166,11 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             const float4* T = S.tris + 4 * tri;
             const float4 t0 = T[0], t1 = T[1], t2 = T[2];
             double t;
+#if RT_MT_PK
+            const bool mh = moller_trumbore_pk(t0, t1, t2, o, d, t);
+#else
             const bool mh = moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o, d, t);
+#endif
 #if RT_SECTIONS
             SEC_COUNT(5, 1u);
             SEC_COUNT(6, (uint32_t)__popcll(__ballot(1)));
@@ -1858,9 +1869,14 @@ __global__ void __launch_bounds__(256) debug_primitives_kernel(uint32_t n_mt, co
     if (i < n_mt) {
         const float* q = mt + 15 * (size_t)i;
         const V3 a{q[0], q[1], q[2]}, b{q[3], q[4], q[5]}, c{q[6], q[7], q[8]}, o{q[9], q[10], q[11]}, d{q[12], q[13], q[14]};
-        double t = 0.0;
-        const bool h = moller_trumbore_od(a, sub(b, a), sub(c, a), o, d, t);
-        mt_hit[i] = h ? 1 : 0;
+        double t = 0.0, tp = 0.0;
+        const V3 e1 = sub(b, a), e2 = sub(c, a);
+        const bool h = moller_trumbore_od(a, e1, e2, o, d, t);
+        // the packed form (moller_trumbore_pk, the leaf-box variant's) must agree bit for bit: 2 flags a difference
+        const bool hp = moller_trumbore_pk(make_float4(a.x, a.y, a.z, 0.0f), make_float4(e1.x, e1.y, e1.z, 0.0f),
+                                           make_float4(e2.x, e2.y, e2.z, 0.0f), o, d, tp);
+        const bool same = h == hp && (!h || __double_as_longlong(t) == __double_as_longlong(tp));
+        mt_hit[i] = same ? (h ? 1 : 0) : 2;
         mt_t[i] = h ? t : 0.0;
     }
     if (i < n_box) {

@@ -401,6 +401,76 @@ __device__ __forceinline__ bool sphere_hit(const V3& c, float r2, const Ray& r, 
 // the scalar instruction, at half the issue cost
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// Moller-Trumbore on packed pairs (round 6, RT_MT_PK, measured slower and off: rt_coherent.hip): moller_trumbore_od's
+// IEEE operations, every product and difference rounded on its own, two of them per v_pk_mul_f32 / v_pk_add_f32
+// (41 -> 29 VALU for the float part).
+// glm::cross(u, v) (GLM/detail/func_geometric.inl:68-80) = (u.y*v.z - v.y*u.z, u.z*v.x - v.z*u.x, u.x*v.y - v.x*u.y):
+//   Q1 = u.z * (v.x, v.y) = (cy's first, cx's second product), Q2 = v.z * (u.y, u.x) = (cx's first, cy's second),
+//   (cx, cy) = (Q2.lo - Q1.hi, Q1.lo - Q2.hi): one v_pk_add_f32 whose op_sel picks the halves and whose
+//   neg_lo / neg_hi negate the subtrahends (RN(a + (-b)) = RN(a - b));  R = (u.x*v.y, u.y*v.x), cz = R.lo - R.hi.
+// glm::dot(a, b) = (a.x*b.x + a.y*b.y) + a.z*b.z, the first two products in one v_pk_mul_f32.  The op_sel forms are
+// inline asm: the compiler materialises broadcasts and swaps with moves instead.
+__device__ __forceinline__ f2 pk_mul_bcast(f2 s, f2 v)        // (s.lo * v.lo, s.lo * v.hi)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(r) : "v"(s), "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_bcast_swap(f2 s, f2 v)   // (s.lo * v.hi, s.lo * v.lo)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,0]" : "=v"(r) : "v"(s), "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 pk_mul_swap(f2 u, f2 v)         // (u.lo * v.hi, u.hi * v.lo)
+{
+    f2 r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(u), "v"(v));
+    return r;
+}
+__device__ __forceinline__ f2 pk_cross_xy(f2 q2, f2 q1)       // (q2.lo - q1.hi, q1.lo - q2.hi)
+{
+    f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(q2), "v"(q1));
+    return r;
+}
+// glm::cross(u, v) for u = (uxy, uz), v = (vxy, vz.lo): (x, y) packed, z alone; vz and uz_b carry their z in .lo
+__device__ __forceinline__ void pk_cross(f2 uxy, f2 uz_b, f2 vxy, f2 vz_b, f2& cxy, float& cz)
+{
+    cxy = pk_cross_xy(pk_mul_bcast_swap(vz_b, uxy), pk_mul_bcast(uz_b, vxy));
+    const f2 r = pk_mul_swap(uxy, vxy);
+    cz = r.x - r.y;
+}
+__device__ __forceinline__ float pk_dot(f2 axy, float az, f2 bxy, float bz)
+{
+    const f2 p = axy * bxy;
+    return (p.x + p.y) + az * bz;
+}
+// moller_trumbore_od with a = t0.xyz, e1 = t1.xyz, e2 = t2.xyz (the .w words only ride in the pairs)
+__device__ __forceinline__ bool moller_trumbore_pk(const float4 t0, const float4 t1, const float4 t2, const V3& o, const V3& d, double& t_out)
+{
+    const f2 dxy{d.x, d.y}, e1xy{t1.x, t1.y}, e2xy{t2.x, t2.y};
+    const f2 e1zw{t1.z, t1.w}, e2zw{t2.z, t2.w};
+    const f2 Sxy = f2{o.x, o.y} - f2{t0.x, t0.y};
+    const float Sz = o.z - t0.z;
+    f2 S1xy, S2xy;
+    float S1z, S2z;
+    pk_cross(dxy, f2{d.z, d.z}, e2xy, e2zw, S1xy, S1z);   // S1 = cross(d, e2)
+    pk_cross(Sxy, f2{Sz, Sz}, e1xy, e1zw, S2xy, S2z);     // S2 = cross(S, e1)
+    const float den = pk_dot(S1xy, S1z, e1xy, t1.z);
+    const float tn = pk_dot(S2xy, S2z, e2xy, t2.z), b2n = pk_dot(S1xy, S1z, Sxy, Sz), b3n = pk_dot(S2xy, S2z, dxy, d.z);
+    const float lo3 = __builtin_fminf(__builtin_fminf(tn, b2n), b3n), hi3 = __builtin_fmaxf(__builtin_fmaxf(tn, b2n), b3n);
+    if (!(lo3 > 0.0f || hi3 < 0.0f)) return false;
+    const float sb = __builtin_fabsf(b2n) + __builtin_fabsf(b3n), aden = __builtin_fabsf(den);
+    if (sb > aden * 1.00001f) return false;
+    const double inv = rcp_f64_of_f32(den);
+    const double t = (double)tn * inv;
+    t_out = t;
+    const double b2 = (double)b2n * inv;
+    const double b3 = (double)b3n * inv;
+    return (t > 0.0) && (((1.0 - b2) - b3) > 0.0);
+}
+
 // cos/sin of the hemisphere angle phi = 2*PI*U in [0, 2*PI] (MC/WhittedMaterial.h:80-81 calls
 // std::cos/std::sin(float) -> glibc cosf/sinf).  Restatement of glibc 2.35's single-precision
 // algorithm (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h; ARM optimized-routines):
