@@ -42,9 +42,7 @@ struct rt_ctx {
     float4* d_worders = nullptr;  // Whitted scenes: near-first orderings of the whole tree (FlatScene::worders)
     uint4* d_worders_h = nullptr; // the same in 16-byte nodes, half planes rounded outward (FlatScene::worders_h)
     uint32_t split_root = 0, split_end = 0, n_sboxes = 0, n_sleaves = 0;
-    uint4* d_qnodes = nullptr;                     // compact BVH (rt_layout.h)
-    float4 *d_tabc = nullptr, *d_tnrm = nullptr;
-    bool qbvh = false;                             // RT_QBVH=1: the BVH variant walks the compact BVH (A/B: slower)
+    float4* d_tabc = nullptr;                      // the triangles' vertices (the Whitted half-plane walk's exact leaf boxes)
     // fold-level materials in the direct term's sign bits (one 16-byte ring entry per level instead of an
     // entry plus a 4-byte material that misses L2 on its own line: C4 221 -> 133 B/sample of L2 -> fabric
     // traffic): RT_RING_PACK 0 off, 1 BVH variant only, 2 both variants
@@ -499,7 +497,6 @@ rt_status rt_create(rt_ctx** out, const rt_device_cfg* cfg)
     if (const char* e = rt_knob("RT_VERTEX_BVH")) c->vertex_bvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_LBUF_PIXEL_MAJOR")) c->lbuf_pm = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_FORCE_WALK")) c->force_walk = std::strtoul(e, nullptr, 10) != 0;
-    if (const char* e = rt_knob("RT_QBVH")) c->qbvh = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_RING_PACK")) c->ring_pack = (uint32_t)std::strtoul(e, nullptr, 10);
     if (const char* e = rt_knob("RT_BVH_PREPASS")) c->bvh_prepass = std::strtoul(e, nullptr, 10) != 0;
     if (const char* e = rt_knob("RT_PRE_DEFER")) c->pre_defer_walk = std::strtoul(e, nullptr, 10) != 0;
@@ -563,7 +560,7 @@ void rt_destroy(rt_ctx* c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders);
     dfree(c->d_nodes); dfree(c->d_tris); dfree(c->d_mats); dfree(c->d_lnodes); dfree(c->d_ltris); dfree(c->d_lboxes); dfree(c->d_wmats); dfree(c->d_plights);
-    dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
+    dfree(c->d_tabc);
     dfree(c->d_went); dfree(c->d_wtris);
     dfree(c->d_gb_color); dfree(c->d_gb_pos); dfree(c->d_gb_nrm); dfree(c->d_spatial); dfree(c->d_temporal); dfree(c->d_prev_color);
     dfree(c->d_gb_prim); dfree(c->d_prev_prim); dfree(c->d_dn_rgba); dfree(c->d_lbuf); dfree(c->d_sky);
@@ -599,7 +596,7 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     if ((r = upload(c, c->d_stri, s->flat.stri)) != RT_OK) return r;
     {   // the near-first orderings (8 x the walked subtree's nodes: 40.7 MB at C5) only where the BVH variant walks them
         static const std::vector<float> kNone;
-        const bool walks = c->vertex && c->vertex_bvh && c->split && c->walk_order && !c->qbvh && !c->force_walk;
+        const bool walks = c->vertex && c->vertex_bvh && c->split && c->walk_order && !c->force_walk;
         if ((r = upload(c, c->d_wcopies, walks ? s->flat.wcopies : kNone)) != RT_OK) return r;
         // (8 x the whole tree's nodes for a Whitted scene: 5.8 MB at C3)
         if ((r = upload(c, c->d_worders, c->wh_order ? s->flat.worders : kNone)) != RT_OK) return r;
@@ -611,9 +608,10 @@ rt_status rt_upload_scene(rt_ctx* c, const rt_scene* s)
     c->split_end = s->flat.split_end;
     c->n_sboxes = (uint32_t)(s->flat.sboxes.size() / 8);
     c->n_sleaves = (uint32_t)s->flat.stri.size();
-    if ((r = upload(c, c->d_qnodes, s->flat.qnodes)) != RT_OK) return r;
-    if ((r = upload(c, c->d_tabc, s->flat.tabc)) != RT_OK) return r;
-    if ((r = upload(c, c->d_tnrm, s->flat.tnrm)) != RT_OK) return r;
+    {   // the vertices, when the Whitted walk takes the half-plane orderings (RT_WH_HALF)
+        static const std::vector<float> kNoneF;
+        if ((r = upload(c, c->d_tabc, c->wh_order && c->wh_half ? s->flat.tabc : kNoneF)) != RT_OK) return r;
+    }
     if ((r = upload(c, c->d_wmats, s->flat.wmats)) != RT_OK) return r;
     if ((r = upload(c, c->d_plights, s->flat.plights)) != RT_OK) return r;
     if ((r = upload(c, c->d_went, s->flat.went)) != RT_OK) return r;
@@ -690,12 +688,12 @@ rt_status rt_upload_scene_gpu_bvh(rt_ctx* c, const rt_scene* s, float* build_ms)
     dfree(c->d_nodes); dfree(c->d_tris);
     c->d_nodes = d_nodes; c->d_tris = d_tris;
     // the BVH-walking kernels: no leaf-box table, no compact tree
-    dfree(c->d_lboxes); dfree(c->d_qnodes); dfree(c->d_tabc); dfree(c->d_tnrm);
+    dfree(c->d_lboxes); dfree(c->d_tabc);
     dfree(c->d_sboxes); dfree(c->d_stri); dfree(c->d_wcopies); dfree(c->d_worders); dfree(c->d_worders_h);   // the split and orderings refer to the host tree's node order
     c->split_root = c->split_end = c->n_sboxes = c->n_sleaves = 0;
     c->hdr.n_nodes = m;
     c->hdr.n_lboxes = 0;
-    c->hdr.has_qnodes = 0;
+    c->hdr.has_vboxes = 0;
     return RT_OK;
 }
 
@@ -773,19 +771,16 @@ rt_status rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, 
     if (c->split && c->split_root != 0 && P.n_lboxes == 0) {
         P.sboxes = c->d_sboxes; P.stri = c->d_stri; P.n_sboxes = c->n_sboxes;
         P.split_root = c->split_root; P.split_end = c->split_end; P.n_split_leaves = c->n_sleaves;
-        // (not with the compact tree or the forced full walk: both walk the original order)
-        if (c->walk_order && c->d_wcopies && !c->qbvh && !c->force_walk) {
+        // (not with the forced full walk: it walks the original order)
+        if (c->walk_order && c->d_wcopies && !c->force_walk) {
             // offset so that node k of an ordering is at [2 * k] (k >= split_root; computed as an integer)
             P.wcopies = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(c->d_wcopies) - (uintptr_t)c->split_root * 2u * sizeof(float4));
             P.wcopy_stride = 2u * (c->split_end - c->split_root);
         }
     }
     P.worders = c->d_worders;
-    P.worders_h = (c->d_worders && c->d_worders_h && c->hdr.has_qnodes && c->d_tabc) ? c->d_worders_h : nullptr;
-    P.qnodes = c->d_qnodes; P.tabc = c->d_tabc; P.tnrm = c->d_tnrm;
-    P.use_qnodes = (c->qbvh && c->hdr.has_qnodes && c->d_qnodes) ? 1u : 0u;
-    std::memcpy(P.q_origin, c->hdr.q_origin, sizeof P.q_origin);
-    std::memcpy(P.q_scale, c->hdr.q_scale, sizeof P.q_scale);
+    P.worders_h = (c->d_worders && c->d_worders_h && c->hdr.has_vboxes && c->d_tabc) ? c->d_worders_h : nullptr;
+    P.tabc = c->d_tabc;
     P.light_area = c->hdr.light_area;
     std::memcpy(P.light_emission, c->hdr.light_emission, sizeof P.light_emission);
     P.has_light = c->hdr.light_mesh >= 0 && c->hdr.n_ltris > 0;

@@ -918,7 +918,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             tri = triA;
             if (BVH) {
                 loc = add(o, smul((float)tA, dA));
-                const float4 tn = kargs4().use_qnodes ? kargs4().tnrm[tri < 0 ? 0 : tri] : S.tris[4 * (tri < 0 ? 0 : tri) + 3];
+                const float4 tn = S.tris[4 * (tri < 0 ? 0 : tri) + 3];
                 flip = dot(V3{tn.x, tn.y, tn.z}, neg(dA)) < 0.0f;
             } else {
                 loc = hloc;
@@ -931,7 +931,7 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
         if (vertex) {
             // ------------ vertex `depth`: Renderer::shading (MC/Renderer.cpp:163-209) up to its two rays
             CKParams& Q = kargs4();
-            const float4 tq3 = (BVH && Q.use_qnodes) ? Q.tnrm[tri] : S.tris[4 * tri + 3];
+            const float4 tq3 = S.tris[4 * tri + 3];
             const V3 N{tq3.x, tq3.y, tq3.z};
             const V3 n = flip ? neg(N) : N;
             const V3 p = add(loc, muls(n, INTERSECTION_CORRECTION));
@@ -1313,9 +1313,6 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                 // across the iteration)
                 const Ray r{o, d, rcp3(d), d.x < 0.0f, d.y < 0.0f, d.z < 0.0f};
                 const bool fin = __all(!tracing || finite3(r.rcp));
-                // compact BVH for an all-finite wave (rt_layout.h): quantized internal boxes (rounded
-                // outward: only extra visits), exact leaf boxes from the triangle's vertices
-                const bool qround = fin && Q.use_qnodes != 0u;
                 // the walk skips a box entered beyond every t that could still matter (exact, DESIGN.md
                 // 5.3): ray A's closest hit so far -- a triangle inside the box hits at t >= its entry, so
                 // it would lose to the current hit (a tie needs entry <= t; the bound keeps 1e-5 relative
@@ -1340,27 +1337,6 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     uint32_t ti2 = pair ? tiB : NN;
                     int park2 = -1;
 #endif
-                    auto walk_q = [&]() {
-                        // every node's quantized box (16 B): an internal hit descends, a leaf hit parks the
-                        // triangle; its exact box is tested with its vertices at the end of the round
-                        const float ox = kargs4().q_origin[0], oy = kargs4().q_origin[1], oz = kargs4().q_origin[2];
-                        const float sx = kargs4().q_scale[0], sy = kargs4().q_scale[1], sz = kargs4().q_scale[2];
-                        const uint4* __restrict__ qn = kargs4().qnodes;
-                        for (uint32_t s = 0; s < steps && ti < tend; ++s) {
-                            const uint4 q = qn[ti];
-                            const float lx = __builtin_fmaf((float)(q.x & 0xFFFFu), sx, ox), hx = __builtin_fmaf((float)(q.x >> 16), sx, ox);
-                            const float ly = __builtin_fmaf((float)(q.y & 0xFFFFu), sy, oy), hy = __builtin_fmaf((float)(q.y >> 16), sy, oy);
-                            const float lz = __builtin_fmaf((float)(q.z & 0xFFFFu), sz, oz), hz = __builtin_fmaf((float)(q.z >> 16), sz, oz);
-                            const bool hit = slab_hit_finite_within(r, lx, ly, lz, hx, hy, hz, bound);
-                            const bool leaf = (q.w & 0x80000000u) != 0u;
-                            ti = (hit && !leaf) ? ti + 1 : (leaf ? ti + 1 : q.w);
-                            if (hit && leaf) {
-                                const int tri = (int)(q.w & 0x7FFFFFFFu);
-                                if (parked0 < 0) parked0 = tri;
-                                else { parked1 = tri; break; }
-                            }
-                        }
-                    };
                     auto walk = [&](auto kind, auto baked) {
                         // a split scene's ray with a finite reciprocal direction walks the subtree from its root:
                         // in the near-first ordering of its direction's octant when the scene has them, whose
@@ -1416,8 +1392,10 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     // (in a wave with a non-finite reciprocal the finite lanes still walk their ordering: a walk's
                     // position spans rounds, and it indexes the ordering; the others walk the DFS array with the
                     // general slab)
-                    if (qround) walk_q();
-                    else if (fin && Q.wcopies != nullptr) walk(FiniteSlab{}, std::true_type{});
+                    // (round 6: the compact 16-bit BVH walk, RT_QBVH, is gone from this kernel -- slower in every
+                    // measurement, and its code cost the variant 2 spilled VGPRs: C5 +2.1 % without it,
+                    // profiles/r06/ab/ab_c5_no_qbvh.json)
+                    if (fin && Q.wcopies != nullptr) walk(FiniteSlab{}, std::true_type{});
                     else if (fin) walk(FiniteSlab{}, std::false_type{});
                     else if (Q.wcopies != nullptr && finite3(r.rcp)) walk(FiniteSlab{}, std::true_type{});
                     else walk(GeneralSlab{}, std::false_type{});
@@ -1428,22 +1406,8 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     for (int slot = 0; slot < 2; ++slot) {
                         const int pk = slot == 0 ? parked0 : parked1;
                         if (pk < 0 || (!curA && occB)) continue;
-                        V3 va, e1, e2;
-                        if (qround) {
-                            const float4* ta = kargs4().tabc + 3 * pk;
-                            const float4 t0 = ta[0], t1 = ta[1], t2 = ta[2];
-                            // the exact leaf box: Triangle::Get3DAABB (MC/TriangleMesh.h:96-99)
-                            if (!slab_hit_finite(r, __builtin_fminf(__builtin_fminf(t0.x, t1.x), t2.x), __builtin_fminf(__builtin_fminf(t0.y, t1.y), t2.y),
-                                                 __builtin_fminf(__builtin_fminf(t0.z, t1.z), t2.z), __builtin_fmaxf(__builtin_fmaxf(t0.x, t1.x), t2.x),
-                                                 __builtin_fmaxf(__builtin_fmaxf(t0.y, t1.y), t2.y), __builtin_fmaxf(__builtin_fmaxf(t0.z, t1.z), t2.z)))
-                                continue;
-                            va = V3{t0.x, t0.y, t0.z};   // e1 = b - a, e2 = c - a: the floats `tris` holds
-                            e1 = sub(V3{t1.x, t1.y, t1.z}, va);
-                            e2 = sub(V3{t2.x, t2.y, t2.z}, va);
-                        } else {
-                            const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
-                            va = V3{t0.x, t0.y, t0.z}; e1 = V3{t1.x, t1.y, t1.z}; e2 = V3{t2.x, t2.y, t2.z};
-                        }
+                        const float4 t0 = S.tris[4 * pk], t1 = S.tris[4 * pk + 1], t2 = S.tris[4 * pk + 2];
+                        const V3 va{t0.x, t0.y, t0.z}, e1{t1.x, t1.y, t1.z}, e2{t2.x, t2.y, t2.z};
                         double t;
                         if (moller_trumbore_od(va, e1, e2, o, d, t)) {
                             if (curA) {

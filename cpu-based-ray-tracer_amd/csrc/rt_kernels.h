@@ -30,10 +30,9 @@ struct KParams {
     const uint4* worders_h;
     // (the BVH variant stages the small tables (mats | lnodes | ltris) in LDS, the split's outside triangles
     //  (3 float4 per slot: a, e1, (e2, bits(triangle))) after them; rt_capi.cpp checks that they fit)
-    // compact BVH (rt_layout.h): quantized internal boxes, leaf boxes from the vertices; the vertex
-    // kernel's BVH variant walks it for waves whose rays all have a finite reciprocal direction
-    const uint4* qnodes; const float4* tabc; const float4* tnrm; uint32_t use_qnodes;
-    float q_origin[3], q_scale[3];
+    // the triangles' vertices, 3 float4 per slot (FlatScene::tabc): the exact leaf boxes of the half-plane walk
+    // (round 6: the vertex kernel's compact-BVH walk, RT_QBVH, is gone)
+    const float4* tabc;
     float light_area; float light_emission[3]; int has_light;
     // Whitted shading (rt_whitted.hip): per-material (diffuse color, phong_diffuse), point lights, sky
     const float4* wmats; const float4* plights; uint32_t n_plights; float sky[3];

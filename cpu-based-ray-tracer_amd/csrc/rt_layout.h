@@ -59,20 +59,13 @@ typedef struct {
     int32_t max_bounce_depth;  // WH/World.h:55
     float intersection_correction;   // WH/World.h:56
     uint32_t n_lboxes;         // distinct leaf boxes of a small scene (<= 64 triangles), 0 otherwise
-    uint32_t has_qnodes;       // the compact BVH below was built (every leaf box is its triangle's vertex box)
-    float q_origin[3], q_scale[3];   // compact BVH plane decode: plane = fmaf((float)q, scale, origin)
+    uint32_t has_vboxes;       // every leaf box is its triangle's vertex box (FlatScene::tabc holds the vertices)
     uint32_t n_spheres;        // sphere entities (their slots in `tris` carry the sphere flag)
 } rt_scene_header;
 
-// Compact BVH (the vertex kernel's BVH variant; rays with a finite reciprocal direction):
-//  qnodes : 4 x u32 per node, the nodes' DFS pre-order of `nodes`
-//             internal: (qlo.x | qhi.x << 16, qlo.y | qhi.y << 16, qlo.z | qhi.z << 16, skip)
-//             leaf    : (the same for its box, 0x80000000 | triangle slot)  (a pre-filter: the exact leaf box
-//                       is its triangle's vertex box, tested after it)
-//           16-bit planes rounded outward: fmaf(qlo, scale, origin) <= lo, fmaf(qhi, scale, origin) >= hi
-//  tabc   : 3 x float4 per triangle slot: (a, bits(material)), (b, bits(primitive id)), (c, 0);
-//           Moller-Trumbore takes e1 = b - a, e2 = c - a (the same correctly rounded floats as `tris`)
-//  tnrm   : 1 x float4 per triangle slot: (n, 0)
+// tabc (when hdr.has_vboxes; the Whitted half-plane walk's exact leaf boxes): 3 x float4 per triangle slot:
+//   (a, bits(material)), (b, bits(primitive id)), (c, 0); Moller-Trumbore takes e1 = b - a, e2 = c - a (the same
+//   correctly rounded floats as `tris`).  (Round 6: the 16-bit compact BVH "qnodes" and its normals are gone.)
 
 // lboxes (small scenes: the vertex kernel's leaf-box trace, the megakernel's coherent trace): 2 float4
 // per distinct leaf box, (lo.x, hi.x, lo.y, hi.y)(lo.z, hi.z, bits of the mask of its triangles 0-31,

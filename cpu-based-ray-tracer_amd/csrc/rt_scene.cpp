@@ -617,7 +617,7 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
     out.lboxes.clear();
     out.hdr.n_lboxes = 0;
     // (scenes with spheres render on the megakernel's BVH walk: no leaf-box trace, split trace, near-first
-    // orderings, compact BVH or light-plane masks, which are all built for triangle leaves)
+    // orderings or light-plane masks, which are all built for triangle leaves)
     if (NT > 0 && NT <= 64 && n_spheres == 0) {
         bool contained = true;
         std::vector<std::pair<Box, uint64_t>> uniq;
@@ -814,87 +814,39 @@ bool SceneBuilder::build(FlatScene& out, std::string& err) const
         d[12] = t.area;
         out.dbg_tri_i[2 * s] = t.mesh; out.dbg_tri_i[2 * s + 1] = t.mesh;
     }
-    // ---- compact BVH for scenes traced from HBM (the vertex kernel's BVH variant, rt_layout.h "qnodes"):
-    // boxes quantized to 16 bits per plane, rounded OUTWARD (a decoded box contains the exact one); a
-    // leaf's exact box is min/max of its triangle's vertices (Triangle::Get3DAABB,
-    // MC/TriangleMesh.h:96-99), recomputed from `tabc` for the leaves whose quantized box passes.  For a ray with a finite
-    // reciprocal direction the slab test is monotone in the box planes and every box contains its
-    // subtree's boxes, so an enlarged internal box only adds visits, never loses a leaf, and the leaf
-    // tests -- exact -- select exactly the reference's candidate triangles.
-    out.qnodes.clear(); out.tabc.clear(); out.tnrm.clear();
-    out.hdr.has_qnodes = 0;
+    // ---- the triangles' vertices by slot (`tabc`), where every leaf's box is its triangle's vertex box
+    // (Triangle::Get3DAABB, MC/TriangleMesh.h:96-99): the Whitted half-plane walk (RT_WH_HALF) stores its boxes
+    // rounded outward and recomputes a hit leaf's exact box from them.  (Round 6: the vertex kernel's 16-bit compact
+    // BVH that also lived here, RT_QBVH, is gone -- slower in every measurement)
+    out.tabc.clear();
+    out.hdr.has_vboxes = 0;
     if (NN > 0 && NT > 0 && n_spheres == 0) {
-        const Box& root = fn[0].box;
-        const float lo3[3] = {root.lo.x, root.lo.y, root.lo.z}, hi3[3] = {root.hi.x, root.hi.y, root.hi.z};
-        float org[3], scl[3];
         bool ok = true;
-        for (int a = 0; a < 3; ++a) {
-            org[a] = lo3[a];
-            float sc = (hi3[a] - lo3[a]) / 65535.0f;
-            for (int k = 0; k < 64 && std::fmaf(65535.0f, sc, org[a]) < hi3[a]; ++k) sc = std::nextafter(sc, INFINITY);
-            ok = ok && std::isfinite(sc) && std::fmaf(65535.0f, sc, org[a]) >= hi3[a];
-            scl[a] = sc;
-        }
-        auto q_down = [&](float v, int a) -> uint32_t {   // largest q with decode(q) <= v
-            if (!(scl[a] > 0.0f)) return 0u;
-            double g = std::floor(((double)v - (double)org[a]) / (double)scl[a]);
-            uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, g));
-            while (q > 0 && std::fmaf((float)q, scl[a], org[a]) > v) --q;
-            while (q < 65535 && std::fmaf((float)(q + 1), scl[a], org[a]) <= v) ++q;
-            if (std::fmaf((float)q, scl[a], org[a]) > v) ok = false;
-            return q;
-        };
-        auto q_up = [&](float v, int a) -> uint32_t {     // smallest q with decode(q) >= v
-            if (!(scl[a] > 0.0f)) return 0u;
-            double g = std::ceil(((double)v - (double)org[a]) / (double)scl[a]);
-            uint32_t q = (uint32_t)std::min(65535.0, std::max(0.0, g));
-            while (q < 65535 && std::fmaf((float)q, scl[a], org[a]) < v) ++q;
-            while (q > 0 && std::fmaf((float)(q - 1), scl[a], org[a]) >= v) --q;
-            if (std::fmaf((float)q, scl[a], org[a]) < v) ok = false;
-            return q;
-        };
-        out.qnodes.resize((size_t)NN * 4);
         for (uint32_t i = 0; i < NN && ok; ++i) {
             const FN& n = fn[i];
-            uint32_t* q = &out.qnodes[4 * (size_t)i];
-            if (n.tri >= 0) {
-                // a leaf: its box must be its triangle's vertex box (checked; else no compact BVH)
-                const Tri& t = *slot_tri[n.tri];
-                auto mn3 = [](float x, float y, float z) { return std::min(std::min(x, y), z); };
-                auto mx3 = [](float x, float y, float z) { return std::max(std::max(x, y), z); };
-                ok = mn3(t.a.x, t.b.x, t.c.x) == n.box.lo.x && mn3(t.a.y, t.b.y, t.c.y) == n.box.lo.y && mn3(t.a.z, t.b.z, t.c.z) == n.box.lo.z &&
-                     mx3(t.a.x, t.b.x, t.c.x) == n.box.hi.x && mx3(t.a.y, t.b.y, t.c.y) == n.box.hi.y && mx3(t.a.z, t.b.z, t.c.z) == n.box.hi.z &&
-                     n.skip == (int)i + 1;
-                const float l[3] = {n.box.lo.x, n.box.lo.y, n.box.lo.z}, h[3] = {n.box.hi.x, n.box.hi.y, n.box.hi.z};
-                for (int a = 0; a < 3; ++a) q[a] = q_down(l[a], a) | (q_up(h[a], a) << 16);   // a pre-filter only
-                q[3] = 0x80000000u | (uint32_t)n.tri;
-            } else {
-                const float l[3] = {n.box.lo.x, n.box.lo.y, n.box.lo.z}, h[3] = {n.box.hi.x, n.box.hi.y, n.box.hi.z};
-                for (int a = 0; a < 3; ++a) q[a] = q_down(l[a], a) | (q_up(h[a], a) << 16);
-                q[3] = (uint32_t)n.skip;
-            }
+            if (n.tri < 0) continue;
+            const Tri& t = *slot_tri[n.tri];
+            auto mn3 = [](float x, float y, float z) { return std::min(std::min(x, y), z); };
+            auto mx3 = [](float x, float y, float z) { return std::max(std::max(x, y), z); };
+            ok = mn3(t.a.x, t.b.x, t.c.x) == n.box.lo.x && mn3(t.a.y, t.b.y, t.c.y) == n.box.lo.y && mn3(t.a.z, t.b.z, t.c.z) == n.box.lo.z &&
+                 mx3(t.a.x, t.b.x, t.c.x) == n.box.hi.x && mx3(t.a.y, t.b.y, t.c.y) == n.box.hi.y && mx3(t.a.z, t.b.z, t.c.z) == n.box.hi.z &&
+                 n.skip == (int)i + 1;
         }
         if (ok) {
             out.tabc.resize((size_t)NT * 12);
-            out.tnrm.resize((size_t)NT * 4);
             for (uint32_t s2 = 0; s2 < NT; ++s2) {
                 const Tri& t = *slot_tri[s2];
                 float* q = &out.tabc[12 * (size_t)s2];
                 q[0] = t.a.x; q[1] = t.a.y; q[2] = t.a.z; q[3] = bits_as_float(t.mesh);
                 q[4] = t.b.x; q[5] = t.b.y; q[6] = t.b.z; q[7] = bits_as_float(t.id);
                 q[8] = t.c.x; q[9] = t.c.y; q[10] = t.c.z; q[11] = 0.0f;
-                float* r = &out.tnrm[4 * (size_t)s2];
-                r[0] = t.n.x; r[1] = t.n.y; r[2] = t.n.z; r[3] = 0.0f;
             }
-            for (int a = 0; a < 3; ++a) { out.hdr.q_origin[a] = org[a]; out.hdr.q_scale[a] = scl[a]; }
-            out.hdr.has_qnodes = 1;
-        } else {
-            out.qnodes.clear();
+            out.hdr.has_vboxes = 1;
         }
     }
     // ---- the Whitted orderings in 16 bytes per node, where the exact leaf test has the vertices (tabc)
     out.worders_h.clear();
-    if (!out.worders.empty() && out.hdr.has_qnodes && !compact_orderings(out.worders, NN, 0u, out.worders_h)) out.worders_h.clear();
+    if (!out.worders.empty() && out.hdr.has_vboxes && !compact_orderings(out.worders, NN, 0u, out.worders_h)) out.worders_h.clear();
     // ---- materials (one per mesh): brdf = diffuse_coefficient / PI, emitting = length(emission) > 1e-5
     const float PI = 3.141592653589793f;   // MC/WhittedUtilities.h:20
     out.mats.resize(nm * 8);

@@ -73,8 +73,7 @@ struct FlatScene {
     // node); built when every leaf's box is its triangle's vertex box (`tabc` holds the vertices for the exact
     // leaf test); empty otherwise
     std::vector<uint32_t> worders_h;
-    std::vector<uint32_t> qnodes;                                         // compact BVH: 4 words per node
-    std::vector<float> tabc, tnrm;                                        // compact BVH: vertices, normals
+    std::vector<float> tabc;   // the triangles' vertices by slot, 3 float4 each (built when hdr.has_vboxes)
     // per-node debug view (tests): box, area, left, right, tri, mesh, top-level flag
     std::vector<float> dbg_node_f;    // 7 per node
     std::vector<int32_t> dbg_node_i;  // 5 per node

@@ -160,14 +160,13 @@ def test_full_frame_digest(ctx, fixture):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"RT_QBVH": "0", "RT_RING_PACK": "0"}, {"RT_QBVH": "0", "RT_RING_PACK": "1"}, {"RT_QBVH": "1", "RT_RING_PACK": "1"},
+@pytest.mark.parametrize("env", [{"RT_RING_PACK": "0"}, {"RT_RING_PACK": "1"},
                                  {"RT_SPLIT": "0"}, {"RT_FORCE_WALK": "1"}, {"RT_THRESH": "0", "RT_STEPS": "1"},
                                  {"RT_THRESH": "64"}, {"RT_BVH_PREPASS": "0"}, {"RT_BVH_PREPASS": "0", "RT_FORCE_WALK": "1"},
                                  {"RT_PRE_DEFER": "0"}, {"RT_WALK_ORDER": "0"}, {"RT_WALK_ORDER": "0", "RT_BVH_PREPASS": "0"}])
 def test_vertex_bvh_variant_bitwise(scene, fixture, env, monkeypatch):
     """The vertex kernel's BVH variant (the C5 path) on the reference's 96x54x16 accumulation, with the
-    fold-level materials in their own array or in the direct term's sign bits, walking the exact
-    nodes or the compact BVH (16-bit outward-rounded boxes, exact leaf boxes from the vertices), and
+    fold-level materials in their own array or in the direct term's sign bits, and
     with the materials and light tables in LDS (default) or read from HBM; the camera rays traced by the
     split scene's pre-pass (default; the rays that enter the walked subtree's box are recorded as camera rays
     and traced by the path kernel, RT_PRE_DEFER=0: walked by the pre-pass) or by the path kernel itself

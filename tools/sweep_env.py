@@ -18,7 +18,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 from _rt import rt  # noqa: E402
 
-KNOBS = ("RT_RING_PACK", "RT_QBVH", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_BVH_PREPASS", "RT_PRE_DEFER", "RT_WALK_TREE", "RT_SKY_BITS", "RT_SAH_BINS", "RT_SEG_MIN_PARTS", "RT_SEG_PART_LF", "RT_SEG_TAIL_PARTS", "RT_SEG_TAIL_EXTRA", "RT_WORK_QUEUES")
+KNOBS = ("RT_RING_PACK", "RT_LBUF_PIXEL_MAJOR", "RT_VERTEX", "RT_VERTEX_BVH", "RT_BRUTE", "RT_FORCE_WALK", "RT_LDS_LEVELS", "RT_LDS_PAD", "RT_THRESH", "RT_STEPS", "RT_CHUNKS", "RT_ITEMS_PER_LANE", "RT_MIN_PX_PER_LANE", "RT_MIN_CHUNK_FRAMES", "RT_SEG_PARTS_OFF", "RT_SPLIT", "RT_WALK_ORDER", "RT_BVH_PREPASS", "RT_PRE_DEFER", "RT_WALK_TREE", "RT_SKY_BITS", "RT_SAH_BINS", "RT_SEG_MIN_PARTS", "RT_SEG_PART_LF", "RT_SEG_TAIL_PARTS", "RT_SEG_TAIL_EXTRA", "RT_WORK_QUEUES")
 
 
 def main():
