@@ -375,20 +375,24 @@ def c5_config(rt, dev_index, stream, spp, fast):
                       "scope": "every 64th row" if bool(z["rows_only"]) else "whole frame",
                       "rmse_vs_ref": float(np.sqrt(np.mean((ca - cb) ** 2))), "bitwise_frac": round(float(same.mean()), 6),
                       "sha_accum_match": sha, "sha_match": bool(sha and same.all())}
-            pm = os.path.join(REPO, "tests", "golden", f"{name}_mid.npz")
-            if os.path.exists(pm):
-                # the same frame's rows halfway between (32, 96, ...): every 32nd row pinned
-                zm = np.load(pm)
-                am, bm = acc[zm["rows"], :, :3], zm["accum_rows"]
-                same_m = np.all(am.view(np.uint32) == bm.view(np.uint32), axis=-1)
-                sha_m = hashlib.sha256(np.ascontiguousarray(acc[zm["rows"]]).tobytes()).hexdigest() == str(zm["sha_accum"])
-                ca = np.concatenate([ca, np.clip(am / np.float32(spp), 0.0, 1.0).astype(np.float64)])
-                cb = np.concatenate([cb, np.clip(bm / np.float32(spp), 0.0, 1.0).astype(np.float64)])
-                same_all = np.concatenate([same.ravel(), same_m.ravel()])
-                parity.update({"fixture": f"tests/golden/{name}.npz + {name}_mid.npz", "rows_checked": int(len(rows) + len(zm["rows"])),
-                               "scope": "every 32nd row", "rmse_vs_ref": float(np.sqrt(np.mean((ca - cb) ** 2))),
-                               "bitwise_frac": round(float(same_all.mean()), 6), "sha_accum_match": bool(sha and sha_m),
-                               "sha_match": bool(sha and sha_m and same_all.all())})
+            # the same frame's other row sets (round 6): rows 32, 96, ... (_mid), 16, 80, ... (_o16), 48, 112, ... (_o48)
+            extra = [x for x in ("_mid", "_o16", "_o48") if os.path.exists(os.path.join(REPO, "tests", "golden", f"{name}{x}.npz"))]
+            if extra:
+                same_all, n_rows, sha_all = [same.ravel()], len(rows), sha
+                for x in extra:
+                    zm = np.load(os.path.join(REPO, "tests", "golden", f"{name}{x}.npz"))
+                    am, bm = acc[zm["rows"], :, :3], zm["accum_rows"]
+                    same_all.append(np.all(am.view(np.uint32) == bm.view(np.uint32), axis=-1).ravel())
+                    sha_all = sha_all and hashlib.sha256(np.ascontiguousarray(acc[zm["rows"]]).tobytes()).hexdigest() == str(zm["sha_accum"])
+                    ca = np.concatenate([ca, np.clip(am / np.float32(spp), 0.0, 1.0).astype(np.float64)])
+                    cb = np.concatenate([cb, np.clip(bm / np.float32(spp), 0.0, 1.0).astype(np.float64)])
+                    n_rows += len(zm["rows"])
+                same_all = np.concatenate(same_all)
+                parity.update({"fixture": f"tests/golden/{name}.npz" + "".join(f" + {name}{x}.npz" for x in extra), "rows_checked": int(n_rows),
+                               "scope": f"every {64 // (1 + len(extra))}th row" if len(extra) in (1, 3) else f"{n_rows} rows",
+                               "rmse_vs_ref": float(np.sqrt(np.mean((ca - cb) ** 2))),
+                               "bitwise_frac": round(float(same_all.mean()), 6), "sha_accum_match": bool(sha_all),
+                               "sha_match": bool(sha_all and same_all.all())})
             break
         return {"workload": f"C5 cornell+c5_mesh {W}x{H} {spp}spp", "triangles": 79520, "msamples_per_s": round(samples / dt / 1e6, 2),
                 "render_s": round(dt, 4), "render_ms_with_finalize": round(st.last_kernel_ms, 3), "passes": passes,

@@ -18,6 +18,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py full_c5    # C5 (Cornell + 79k-triangle bunny) at 3840x2160x256 (~10 min)
     python oracle/gen_golden.py full_c5_4096  # C5 at its full 4096 spp, every 64th row (~10 min)
     python oracle/gen_golden.py full_c5_4096_mid  # the same frame's rows 32, 96, ... (round 6)
+    python oracle/gen_golden.py full_c5_4096_o16  # ... rows 16, 80, ...; full_c5_4096_o48: rows 48, 112, ... (round 6)
 """
 import os
 import subprocess
@@ -366,7 +367,7 @@ def gen_full_c5(spp=256, row_stride=1, row_offset=0):
     acc = np.fromfile(tmp("acc"), "<f4").reshape(H, W, 4)
     rgba = np.fromfile(tmp("rgba"), "<u4").reshape(H, W)
     rows = np.arange(row_offset, H, C5_FULL_ROW_STRIDE)
-    name = ("full_c5" if spp == 256 else f"full_c5_{spp}") + ("_mid" if row_offset else "")
+    name = ("full_c5" if spp == 256 else f"full_c5_{spp}") + ({0: "", 32: "_mid"}.get(row_offset, f"_o{row_offset}"))
     # (rows only: the SHA-256 of the committed rows' accumulation and RGBA8 instead of the whole frame's)
     sel_acc, sel_rgba = (acc, rgba) if row_stride == 1 else (np.ascontiguousarray(acc[rows]), np.ascontiguousarray(rgba[rows]))
     np.savez_compressed(os.path.join(GOLDEN, f"{name}.npz"), W=np.int64(W), H=np.int64(H), spp=np.int64(spp),
@@ -740,6 +741,9 @@ def main():
             gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE)
         if only == "full_c5_4096_mid":
             gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=C5_FULL_ROW_STRIDE // 2)
+        if only in ("full_c5_4096_o16", "full_c5_4096_o48"):
+            # the rows a quarter of the stride off (16, 80, ... and 48, 112, ...): with full_c5_4096 and _mid, every 16th row
+            gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=int(only[-2:]))
     print("golden fixtures written to", GOLDEN)
 
 

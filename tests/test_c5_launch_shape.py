@@ -13,8 +13,8 @@ for paths longer than one engine fill (oracle/ref/mt_inject.h) -- via `oracle/ge
 the SHA-256 of the float4 accumulation and of the RGBA8 frame, and every 64th accumulation row.
 tests/golden/full_c5_4096.npz is the same at C5's full 4096 spp on every 64th row (`gen_golden.py full_c5_4096`:
 the harness renders only those rows -- the whole frame would take ~11 h on 8 cores); its SHA-256 covers those
-rows.  tests/golden/full_c5_4096_mid.npz (round 6) holds the rows halfway between (32, 96, ...), so the 4096-spp
-frame is pinned on every 32nd row.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
+rows.  tests/golden/full_c5_4096_mid.npz, _o16.npz and _o48.npz (round 6) hold the rows 32, 96, ..., 16, 80, ... and
+48, 112, ..., so the 4096-spp frame is pinned on every 16th row.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
 the default budget) and compares the rows of both."""
 import hashlib
 import os
@@ -26,6 +26,8 @@ import _oracle as O
 from _rt import rt
 
 FIXTURES = [n for n in ("full_c5", "full_c5_4096") if os.path.exists(os.path.join(O.GOLDEN, f"{n}.npz"))]
+EXTRA_4096 = ("full_c5_4096_mid", "full_c5_4096_o16", "full_c5_4096_o48")
+ROW_OFFSET = {"full_c5_4096_mid": 32, "full_c5_4096_o16": 16, "full_c5_4096_o48": 48}
 
 
 def bits(a):
@@ -45,13 +47,13 @@ def scene(bunny_raw):
 
 def test_fixture_present_and_shaped():
     assert "full_c5" in FIXTURES
-    for name in FIXTURES + ["full_c5_4096_mid"]:
+    for name in FIXTURES + list(EXTRA_4096):
         if not os.path.exists(os.path.join(O.GOLDEN, f"{name}.npz")):
             continue
         z = np.load(os.path.join(O.GOLDEN, f"{name}.npz"))
         W, H, spp = int(z["W"]), int(z["H"]), int(z["spp"])
         assert (W, H, int(z["seed"]), int(z["first_frame"])) == (3840, 2160, 0, 1) and spp in (256, 4096)
-        assert np.array_equal(z["rows"], np.arange(32 if name.endswith("_mid") else 0, H, 64))
+        assert np.array_equal(z["rows"], np.arange(ROW_OFFSET.get(name, 0), H, 64))
         assert z["accum_rows"].shape == (len(z["rows"]), W, 3)
         assert np.all((z["rgba_rows"] >> 24) == 255)
         # samples; no harness overflow (every path read the injected stream, however long)
@@ -103,8 +105,9 @@ def test_c5_frame_in_launch_shape(scene, monkeypatch, name, budget_mb, min_passe
     finally:
         c.close()
     zs = [z]
-    if name == "full_c5_4096" and os.path.exists(os.path.join(O.GOLDEN, "full_c5_4096_mid.npz")):
-        zs.append(np.load(os.path.join(O.GOLDEN, "full_c5_4096_mid.npz")))   # the same frame's rows 32, 96, ... (round 6)
+    if name == "full_c5_4096":
+        # the same frame's rows 32, 96, ... and 16, 80, ... / 48, 112, ... (round 6): every 16th row
+        zs += [np.load(os.path.join(O.GOLDEN, f"{x}.npz")) for x in EXTRA_4096 if os.path.exists(os.path.join(O.GOLDEN, f"{x}.npz"))]
     for z in zs:
         rows = acc[z["rows"], :, :3]
         same = np.all(bits(rows) == bits(z["accum_rows"]), axis=-1)
