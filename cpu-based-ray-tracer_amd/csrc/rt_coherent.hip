@@ -1598,8 +1598,13 @@ __device__ __forceinline__ void walk_subtree(const SceneView& S, const Ray& r, u
     }
 }
 
+// waves per SIMD the leaf-box pre-pass's registers are sized for (0: the compiler's choice, 7 at 67 VGPRs; 8 -- 64 VGPRs,
+// 2 spilled, 42 SGPRs spilled -- pre-pass 15.25 -> 16.06 ms at C4, profiles/r06/ab/ab_c4_prepass_8waves.json)
+#ifndef RT_COH_PRE_WAVES
+#define RT_COH_PRE_WAVES 0
+#endif
 template <bool BVH>
-__global__ void __launch_bounds__(256) camera_prepass_kernel(KParams P)
+__global__ void __launch_bounds__(256, (!BVH && RT_COH_PRE_WAVES) ? RT_COH_PRE_WAVES : 1) camera_prepass_kernel(KParams P)
 {
     extern __shared__ __attribute__((aligned(16))) float4 lds_scene[];
     SceneView S;
