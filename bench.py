@@ -289,11 +289,12 @@ C5_WORK = (3.660, 31.30, 3.85)   # rays per sample, node tests per ray, triangle
 C5_FLOPS_PER_SAMPLE = C5_WORK[0] * (C5_WORK[1] * 18 + C5_WORK[2] * 54) + 0.4036 * C5_WORK[0] * 150
 
 
-def c5_counters(kname, W, H, spp, passes, digest):
-    """The PMC summary of a rocprofv3 pass of this build on C5's frame: the exact shape if one is committed,
-    else the same frame at another spp (the counters are per sample; frames are i.i.d.)."""
+def c5_counters(kname, W, H, spp, passes, digest, mode="exact"):
+    """The PMC summary of a rocprofv3 pass of this build on this frame (C5, or C2 / C3 with mode "whitted"): the
+    exact shape if one is committed, else the same frame at another spp (the counters are per sample; frames are
+    i.i.d.)."""
     import glob
-    exact, other = f"{kname}:{W}x{H}x{spp}_exact_n1_p{passes}", f"{kname}:{W}x{H}x"
+    exact, other = f"{kname}:{W}x{H}x{spp}_{mode}_n1_p{passes}", f"{kname}:{W}x{H}x"
     best = None
     for p in sorted(glob.glob(os.path.join(REPO, "profiles", "r*", "**", "pmc_summary*.json"), recursive=True), reverse=True):
         try:
@@ -301,7 +302,7 @@ def c5_counters(kname, W, H, spp, passes, digest):
         except Exception:
             continue
         k = d.get("key") or ""
-        if digest is None or d.get("lib_sha256") != digest or not k.startswith(other) or "_exact_n1_" not in k:
+        if digest is None or d.get("lib_sha256") != digest or not k.startswith(other) or f"_{mode}_n1_" not in k:
             continue
         d["_file"] = os.path.relpath(p, REPO)
         if k == exact:
@@ -449,9 +450,17 @@ def small_config(rt, dev_index, stream, which, reps=5):
         samples = W * H * spp
         dt, km = float(np.median(wall)), float(np.median(kern))
         achieved = fps * samples / (km / 1e3) / 1e12
+        kname = rt.KERNEL_NAMES.get(st.kernel, str(st.kernel))
         roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / VALU_PEAK_TFLOPS, 4), "kernel": rt.KERNEL_NAMES.get(st.kernel, str(st.kernel)),
-                "kernel_ms": round(km, 3), "flops_per_sample": round(fps, 1)}
+                "frac": round(achieved / VALU_PEAK_TFLOPS, 4), "kernel": kname,
+                "kernel_ms": round(km, 3), "flops_per_sample": round(fps, 1), "counters": None}
+        digest = lib_digest(os.path.join(REPO, "cpu-based-ray-tracer_amd", "librt_hip.so"))
+        pmc = c5_counters(kname, W, H, spp, int(st.n_passes), digest, "exact" if which == "c2" else "whitted")
+        if pmc is not None:
+            roof["counters"] = {"file": pmc["_file"], "profiled_key": pmc.get("key"), "hbm_bytes_per_sample": pmc.get("hbm_bytes_per_sample"),
+                                "valu_issue_frac": pmc.get("valu_issue_frac"), "valu_lane_utilization": pmc.get("valu_lane_utilization"),
+                                "wait_any_frac": pmc.get("wait_any_frac"), "l2_hit_rate": pmc.get("l2_hit_rate"),
+                                "valu_wave_insts_per_sample": pmc.get("valu_wave_insts_per_sample")}
         rgba, acc = ctx.render(cam, spp, fetch=True, **kw)   # the parity render (host copies; not timed)
         parity = None
         if which == "c2":
