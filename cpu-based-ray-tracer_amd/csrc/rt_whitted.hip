@@ -42,6 +42,27 @@ namespace {
 struct FiniteSlab { static constexpr bool value = true; };
 struct GeneralSlab { static constexpr bool value = false; };
 
+// scalar loads of wave-uniform data (constant address space)
+typedef float box8 __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) box8 cbox8;
+typedef float vec4f __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) vec4f cf4;
+
+// the packet walk (round 6): a wave whose rays all have finite reciprocals and one direction octant walks the
+// octant's near-first ordering TOGETHER -- one wave-uniform node index, each node one scalar load for the whole
+// wave (s_load: the vector memory pipeline, which the per-lane walk's 64 gathers per step occupy, is not used),
+// every lane testing it against its own ray and bound; the wave descends when any lane enters the box, and a
+// leaf's triangle (scalar loads too) is intersected by the lanes whose own test entered the leaf's box.  Exact:
+// a lane's tests are its own slab tests on the reference's planes, and a box inside one the lane missed (or
+// entered beyond its bound) is missed too (the finite slab test is monotone, the entry only grows), so each
+// lane intersects exactly the leaves its own walk would, and the closest hit is taken by (min t, max triangle)
+// whatever the order.  Measured (bitwise, the C3 tests green): 14,835 -> 11,004 Msamples/s (profiles/r06/ab/
+// ab_c3_packet_walk.json) -- a scalar load that misses the small scalar cache waits on L2 every step, longer than the
+// per-lane gathers' vL1D hits, and the wave walks the union of its lanes' paths; off.
+#ifndef RT_WH_PACKET
+#define RT_WH_PACKET 0
+#endif
+
 // closest hit (shadow == false) or "any hit with t*t < d2" (shadow == true) over the global scene
 template <bool COUNT>
 __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r, bool shadow, double d2, double& best, int& best_tri, bool& occluded,
@@ -152,6 +173,37 @@ __device__ __forceinline__ void whitted_traverse(const KParams& P, const Ray& r,
             if (p1 >= 0 && tri_test(p1)) return;
         }
     };
+#if RT_WH_PACKET
+    if (P.worders != nullptr) {
+        const uint32_t oct = (uint32_t)r.nx | ((uint32_t)r.ny << 1) | ((uint32_t)r.nz << 2);
+        const uint32_t oct0 = __builtin_amdgcn_readfirstlane(oct);
+        if (__all(rcp_finite(r) && oct == oct0)) {
+            cbox8* wn = (cbox8*)(P.worders + 2u * n * oct0);
+            cf4* ctris = (cf4*)tris;
+            bool live = true;   // a shadow ray stops at its first blocker
+            uint32_t i = 0;
+            while (i < n) {
+                const box8 q = wn[i];
+                const int tri = f2i(q.s7);
+                const uint32_t skip = (uint32_t)f2i(q.s6);
+                const float bound = shadow ? sbound : ((best < 1e30) ? (float)best * 1.00001f + 1e-5f : __builtin_inff());
+                if (COUNT && live) ++node_tests;
+                const bool hit = live && slab_nf_within(r, q.s0, q.s1, q.s2, q.s3, q.s4, q.s5, bound);
+                if (tri >= 0) {
+                    if (hit) {
+                        const vec4f t0 = ctris[4 * tri], t1 = ctris[4 * tri + 1], t2 = ctris[4 * tri + 2];
+                        if (tri_test_v(tri, V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z})) live = false;
+                    }
+                    i = skip;
+                } else {
+                    i = __any(hit) ? i + 1 : skip;
+                }
+                if (shadow && !__any(live)) break;
+            }
+            return;
+        }
+    }
+#endif
     if (!rcp_finite(r)) walk(GeneralSlab{}, std::false_type{});
     else if (RT_WH_HALF && P.worders_h != nullptr) walk_half();
     else if (P.worders != nullptr) walk(FiniteSlab{}, std::true_type{});

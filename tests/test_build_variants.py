@@ -2,7 +2,8 @@
 timing diagnostics (RT_SECTIONS=1 and the candidate-histogram level 3, tools/prof_one.py) and the
 waves-per-SIMD settings measured in DESIGN.md 6.4, the round-4 A/B switches (the drain without the pending
 fold, the BVH variant's division kind, the zero-numerator short division) and the round-6 ones (the C5 A + B pair walk,
-the walk fallback with the sphere branch; in rt_whitted.hip the shadow-ray pair walk and the half-plane orderings).  The product build is the Makefile's; these compile
+the walk fallback with the sphere branch; in rt_whitted.hip the shadow-ray pair walk, the half-plane orderings and
+the packet walk).  The product build is the Makefile's; these compile
 rt_coherent.hip alone, device code only, so a diagnostic that is not built by default cannot rot."""
 import os
 import shutil
@@ -19,7 +20,8 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 @pytest.mark.parametrize("flags", ["-DRT_SECTIONS=1", "-DRT_SECTIONS=3", "-DRT_COH_MIN_WAVES=7 -DRT_COH_BVH_MIN_WAVES=7",
                                    "-DRT_PEND_FOLD=0 -DRT_COH_BVH_PRE_MIN_WAVES=8",
                                    "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0", "-DRT_BVH_PAIR=1 -DRT_COH_SPH=1",
-                                   "@rt_whitted.hip -DRT_WH_PAIR=1 -DRT_WH_WAVES=6", "@rt_whitted.hip -DRT_WH_HALF=1"])
+                                   "@rt_whitted.hip -DRT_WH_PAIR=1 -DRT_WH_WAVES=6", "@rt_whitted.hip -DRT_WH_HALF=1",
+                                   "@rt_whitted.hip -DRT_WH_PACKET=1"])
 def test_coherent_kernel_variant_compiles(flags, tmp_path):
     cmd = [HIPCC, "-std=c++20", "-O3", "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), "-ffp-contract=off",
            "-fno-fast-math", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
