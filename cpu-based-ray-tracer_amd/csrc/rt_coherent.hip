@@ -283,6 +283,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // VALU fewer): C4 -3.3 %, bitwise (profiles/r06/ab/ab_c4_mt_packed.json) -- a v_pk_*_f32 of a wave64 occupies the
 // SIMD twice as long as the scalar instruction on gfx950, so packing buys no issue cycles, and the build spills 2
 // VGPRs; off (debug_primitives_kernel still checks the packed form against moller_trumbore_od bit for bit)
+// the shadow ray's candidates tested from the last DFS triangle down (RT_B_TOP_FIRST=1; any order gives the verdict):
+// C4 12,148 -> 11,803, C2 6762 -> 6564, bitwise (profiles/r06/ab/ab_c{4,2}_b_top_first.json) -- the DFS order already
+// meets the Cornell blocks' faces first; off
+#ifndef RT_B_TOP_FIRST
+#define RT_B_TOP_FIRST 0
+#endif
 #ifndef RT_MT_PK
 #define RT_MT_PK 0
 #endif
@@ -1191,8 +1197,15 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
             // C4 -1 % at caps 6-10 and -10 % at 4: the carried state costs spills, profiles/r03/ab/)
             uint64_t cm = ca | (cb << 32);
             while (cm != 0) {
+#if RT_B_TOP_FIRST
+                // ray A's candidates in DFS order (its tie rule), then ray B's from the LAST triangle down: a shadow
+                // verdict is any blocking hit, the same in any order, and a lane stops at its first blocker
+                const uint32_t bit = ((uint32_t)cm != 0u) ? (uint32_t)__builtin_ctzll(cm) : 63u - (uint32_t)__builtin_clzll(cm);
+                cm &= ~(1ull << bit);
+#else
                 const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
                 cm &= cm - 1;
+#endif
                 test(bit < 32u, (int)(bit & 31u), cm);
             }
         } else {
