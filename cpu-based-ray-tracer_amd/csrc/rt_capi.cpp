@@ -1325,6 +1325,61 @@ rt_status rt_trace(rt_ctx* c, uint64_t n, const float* org, const float* dir, in
     return RT_OK;
 }
 
+#if RT_WALK_STUDY
+// the walk study (variant builds only, rt_kernels.hip walk_study_kernel): n rays walked through the split subtree's
+// near-first orderings, K rays per lane, `steps` node tests per round; `reps` timed launches, their times in ms[]
+rt_status rt_debug_walk_study(rt_ctx* c, uint64_t n, const float* org, const float* dir, uint32_t k, uint32_t steps, uint32_t reps,
+                              int32_t* tri, double* t, float* ms, uint64_t* rounds)
+{
+    // k: rays per lane (1-4), | 0x100 for the refill kernel; 0x201: the (ray, round) count of a K = 1 lockstep run into
+    // rounds[0] (its ms are not a rate)
+    if (!c || !org || !dir || !tri || !t || !ms || n == 0 || n > 0x7FFFFFFFull || (k & 0xFFu) < 1 || (k & 0xFFu) > 4 ||
+        ((k & ~0x1FFu) && k != 0x201u) || steps == 0 || reps == 0 || (k == 0x201u && !rounds))
+        return RT_ERR_INVALID;
+    if (!c->has_scene || c->split_root == 0 || !c->d_wcopies) { c->err = "the walk study needs a split scene with near-first orderings"; return RT_ERR_STATE; }
+    HIPC(c, hipSetDevice(c->device));
+    float *d_o = nullptr, *d_d = nullptr; int32_t* d_tri = nullptr; double* d_t = nullptr; uint32_t* d_ctr = nullptr;
+    auto cleanup = [&]() { dfree(d_o); dfree(d_d); dfree(d_tri); dfree(d_t); dfree(d_ctr); };
+    hipError_t e;
+    if ((e = hipMalloc((void**)&d_o, n * 12)) != hipSuccess || (e = hipMalloc((void**)&d_d, n * 12)) != hipSuccess ||
+        (e = hipMalloc((void**)&d_tri, n * 4)) != hipSuccess || (e = hipMalloc((void**)&d_t, n * 8)) != hipSuccess ||
+        (e = hipMalloc((void**)&d_ctr, 512)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "hipMalloc(rt_debug_walk_study)");
+    }
+    KParams P{};
+    P.nodes = c->d_nodes; P.n_nodes = c->hdr.n_nodes; P.tris = c->d_tris; P.n_tris = c->hdr.n_tris;
+    P.split_root = c->split_root; P.split_end = c->split_end; P.steps = steps;
+    P.wcopies = reinterpret_cast<const float4*>(reinterpret_cast<uintptr_t>(c->d_wcopies) - (uintptr_t)c->split_root * 2u * sizeof(float4));
+    P.wcopy_stride = 2u * (c->split_end - c->split_root);
+    P.counters = reinterpret_cast<decltype(P.counters)>(d_ctr);   // the refill kernel's ray counter
+    if ((e = hipMemcpyAsync(d_o, org, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(d_d, dir, n * 12, hipMemcpyHostToDevice, c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_debug_walk_study");
+    }
+    for (uint32_t r = 0; r < reps; ++r) {
+        if ((e = hipMemsetAsync(d_ctr, 0, 512, c->stream)) != hipSuccess || (e = hipEventRecord(c->ev0, c->stream)) != hipSuccess ||
+            (e = rt_launch_walk_study(P, (uint32_t)n, k, d_o, d_d, d_tri, d_t, c->stream)) != hipSuccess ||
+            (e = hipEventRecord(c->ev1, c->stream)) != hipSuccess || (e = hipEventSynchronize(c->ev1)) != hipSuccess ||
+            (e = hipEventElapsedTime(&ms[r], c->ev0, c->ev1)) != hipSuccess) {
+            cleanup(); return hip_fail(c, e, "rt_debug_walk_study");
+        }
+    }
+    uint64_t cnt[64] = {};
+    if ((e = hipMemcpyAsync(tri, d_tri, n * 4, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(t, d_t, n * 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(cnt, d_ctr, 512, hipMemcpyDeviceToHost, c->stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        cleanup(); return hip_fail(c, e, "rt_debug_walk_study");
+    }
+    if (k == 0x201u) {
+        rounds[0] = 0;
+        for (int i = 0; i < 8; ++i) rounds[0] += cnt[8 * i];
+    }
+    cleanup();
+    return RT_OK;
+}
+#endif
+
 rt_status rt_sample_light(rt_ctx* c, uint64_t n, const uint32_t* u, float* loc, float* normal, float* emission, float* pdf)
 {
     if (!c || (n && (!u || !loc || !normal || !emission || !pdf))) return RT_ERR_INVALID;

@@ -148,6 +148,9 @@ hipError_t rt_launch_debug_primitives(uint32_t n_mt, const float* mt, int32_t* m
                                       int32_t* box_hit, hipStream_t stream);
 hipError_t rt_launch_finalize_chunks(const KParams& P, uint32_t n_px, hipStream_t stream);
 hipError_t rt_launch_trace(const KParams& P, uint32_t n, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
+#if RT_WALK_STUDY
+hipError_t rt_launch_walk_study(const KParams& P, uint32_t n, uint32_t k, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream);
+#endif
 // SamplingAreaLight on given draws (3 u32 per case): out = 10 floats per case (location, normal, emission, PDF)
 hipError_t rt_launch_light_sample(const KParams& P, uint32_t n, const uint32_t* u, float* out, hipStream_t stream);
 hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t stream);

@@ -744,3 +744,254 @@ hipError_t rt_launch_math(uint32_t n, const float* x, float* out, hipStream_t st
     hipLaunchKernelGGL(math_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, n, x, out);
     return hipGetLastError();
 }
+
+#if RT_WALK_STUDY
+// ---------------------------------------------------------------------------------------------
+// Walk study (a variant build only: make KFLAGS=-DRT_WALK_STUDY=1, tools/walk_study.py; the product library has
+// none of it).  The C5 path kernel's BVH rounds (rt_coherent.hip, the split scene's near-first walk of the subtree
+// [split_root, split_end)) lifted into a kernel of their own whose lane carries K independent rays: per step every
+// active ray's node load is issued before any is tested, so a lane keeps K dependent loads in flight instead of one.
+// A round is `steps` node tests per ray, a ray parks up to two leaves and stops stepping for the round at the second,
+// and the parked leaves are intersected at the round's end (the path kernel's round shape).  Closest hit within the
+// subtree by (min t, max triangle) from t = +inf (MC/BVH.h:82-101 restricted to the subtree; equal to rt_trace's
+// result whenever that lies in the subtree).  Ray k of wave w's lane l is ray (w * K + k) * 64 + l: each of a
+// lane's slots is a run of 64 consecutive rays.
+template <int K, bool COUNT = false>
+__global__ void __launch_bounds__(256, K <= 2 ? 8 : 1) walk_study_kernel(KParams P, uint32_t n, const float* __restrict__ org, const float* __restrict__ dir,
+                                                         int32_t* __restrict__ tri_out, double* __restrict__ t_out)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t NN = P.n_nodes, root = P.split_root, tend = P.split_end, steps = P.steps;
+    V3 o[K], d[K], rc[K];
+    uint32_t ti[K], oct[K];
+    double tA[K];
+    int triA[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t i = (wave * (uint32_t)K + (uint32_t)k) * 64u + lane;
+        const bool ok = i < n;
+        const uint32_t j = ok ? i : 0u;
+        o[k] = V3{org[3 * j], org[3 * j + 1], org[3 * j + 2]};
+        d[k] = V3{dir[3 * j], dir[3 * j + 1], dir[3 * j + 2]};
+        rc[k] = V3{rcp_f32(d[k].x), rcp_f32(d[k].y), rcp_f32(d[k].z)};
+        const bool fin = __builtin_isfinite(rc[k].x) && __builtin_isfinite(rc[k].y) && __builtin_isfinite(rc[k].z);
+        ti[k] = (ok && fin) ? root : NN;
+        oct[k] = ((uint32_t)(d[k].x < 0.0f) | ((uint32_t)(d[k].y < 0.0f) << 1) | ((uint32_t)(d[k].z < 0.0f) << 2)) * P.wcopy_stride;
+        tA[k] = 1.7976931348623157e308;
+        triA[k] = (ok && !fin) ? -2 : -1;   // -2: a non-finite reciprocal direction (not walked here)
+    }
+    uint32_t rounds = 0;   // COUNT: the lane's (ray, round) pairs
+    for (;;) {
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            any |= ti[k] < tend;
+            if (COUNT) rounds += ti[k] < tend ? 1u : 0u;
+        }
+        if (!any) break;
+        int p0[K], p1[K];
+        float bnd[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            p0[k] = -1; p1[k] = -1;
+            bnd[k] = (tA[k] < 1e30) ? (float)tA[k] * 1.00001f + 1e-5f : __builtin_inff();
+        }
+        for (uint32_t s = 0; s < steps; ++s) {
+            bool go[K], anyg = false;
+            float4 q0[K], q1[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                go[k] = ti[k] < tend && p1[k] < 0;
+                anyg |= go[k];
+            }
+            if (!anyg) break;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {   // every slot's load first (an idle slot reads the subtree root)
+                const float4* wn = P.wcopies + oct[k];
+                const uint32_t at = 2u * (go[k] ? ti[k] : root);
+                q0[k] = wn[at];
+                q1[k] = wn[at + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!go[k]) continue;
+                const Ray r{o[k], d[k], rc[k], false, false, false};
+                const bool hit = slab_nf_within(r, q0[k].x, q0[k].y, q0[k].z, q0[k].w, q1[k].x, q1[k].y, bnd[k]);
+                const int tri = f2i(q1[k].w);
+                ti[k] = (hit && tri < 0) ? ti[k] + 1u : (uint32_t)f2i(q1[k].z);
+                if (hit && tri >= 0) {
+                    if (p0[k] < 0) p0[k] = tri;
+                    else p1[k] = tri;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            for (int slot = 0; slot < 2; ++slot) {
+                const int pk = slot == 0 ? p0[k] : p1[k];
+                if (pk < 0) continue;
+                const float4 t0 = P.tris[4 * pk], t1 = P.tris[4 * pk + 1], t2 = P.tris[4 * pk + 2];
+                double t;
+                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o[k], d[k], t))
+                    if (t < tA[k] || (t == tA[k] && (uint32_t)pk > (uint32_t)triA[k])) { tA[k] = t; triA[k] = pk; }
+            }
+            if (ti[k] >= tend) ti[k] = NN;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t i = (wave * (uint32_t)K + (uint32_t)k) * 64u + lane;
+        if (i < n) {
+            tri_out[i] = triA[k];
+            t_out[i] = triA[k] >= 0 ? tA[k] : 1.7976931348623157e308;
+        }
+    }
+    if (COUNT) {
+        for (int off = 32; off >= 1; off >>= 1) rounds += (uint32_t)__shfl_xor((int)rounds, off);
+        if (lane == 0) atomicAdd(&P.counters[8u * (blockIdx.x & 7u)], (unsigned long long)rounds);   // (64 B apart)
+    }
+}
+
+// the same walk with refill: a persistent grid whose lanes take a new ray into a slot as soon as the slot's ray is done
+// (one atomic per wave and slot: the wave's free slots counted by ballot, their rays numbered by mbcnt), so a lane's K
+// slots do not wait for the longest of their rays
+template <int K>
+__global__ void __launch_bounds__(256, K <= 1 ? 8 : 1) walk_study_refill_kernel(KParams P, uint32_t n, const float* __restrict__ org, const float* __restrict__ dir,
+                                                                int32_t* __restrict__ tri_out, double* __restrict__ t_out, uint32_t* __restrict__ next_ray)
+{
+    const uint32_t NN = P.n_nodes, root = P.split_root, tend = P.split_end, steps = P.steps;
+    V3 o[K], d[K], rc[K];
+    uint32_t ti[K], oct[K], id[K];
+    double tA[K];
+    int triA[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) { id[k] = 0xFFFFFFFFu; ti[k] = NN; }
+    // the rays in 8 contiguous parts, one counter each (64 B apart), a block's part its blockIdx mod 8; a wave takes
+    // CHUNK rays per atomic into a wave-uniform local range [qb, qe) and refills its free slots from it
+    constexpr uint32_t CHUNK = 256;
+    const uint32_t part = blockIdx.x & 7u;
+    const uint32_t lo = (uint32_t)((uint64_t)n * part / 8u), hi = (uint32_t)((uint64_t)n * (part + 1u) / 8u);
+    uint32_t* ctr = next_ray + 16u * part;
+    uint32_t qb = 0, qe = 0;
+    bool more = true;
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (more) {
+                const bool need = id[k] == 0xFFFFFFFFu;
+                const uint64_t m = __ballot(need);
+                if (m != 0) {
+                    if (qb == qe) {
+                        uint32_t b = 0;
+                        if (__lane_id() == (uint32_t)__builtin_ctzll(m)) b = atomicAdd(ctr, CHUNK);
+                        b = lo + (uint32_t)__shfl((int)b, (int)__builtin_ctzll(m));
+                        if (b >= hi) more = false;
+                        else { qb = b; qe = min(b + CHUNK, hi); }
+                    }
+                    const uint32_t rank = (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull)), avail = qe - qb;
+                    const uint32_t my = qb + rank;
+                    qb += min(avail, (uint32_t)__popcll(m));
+                    if (need && rank < avail) {
+                        id[k] = my;
+                        o[k] = V3{org[3 * my], org[3 * my + 1], org[3 * my + 2]};
+                        d[k] = V3{dir[3 * my], dir[3 * my + 1], dir[3 * my + 2]};
+                        rc[k] = V3{rcp_f32(d[k].x), rcp_f32(d[k].y), rcp_f32(d[k].z)};
+                        const bool fin = __builtin_isfinite(rc[k].x) && __builtin_isfinite(rc[k].y) && __builtin_isfinite(rc[k].z);
+                        ti[k] = fin ? root : NN;
+                        oct[k] = ((uint32_t)(d[k].x < 0.0f) | ((uint32_t)(d[k].y < 0.0f) << 1) | ((uint32_t)(d[k].z < 0.0f) << 2)) * P.wcopy_stride;
+                        tA[k] = 1.7976931348623157e308;
+                        triA[k] = fin ? -1 : -2;
+                    }
+                }
+            }
+        }
+        bool busy = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) busy |= id[k] != 0xFFFFFFFFu;
+        if (!__any(busy)) break;
+        int p0[K], p1[K];
+        float bnd[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            p0[k] = -1; p1[k] = -1;
+            bnd[k] = (tA[k] < 1e30) ? (float)tA[k] * 1.00001f + 1e-5f : __builtin_inff();
+        }
+        for (uint32_t s = 0; s < steps; ++s) {
+            bool go[K], anyg = false;
+            float4 q0[K], q1[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                go[k] = ti[k] < tend && p1[k] < 0;
+                anyg |= go[k];
+            }
+            if (!anyg) break;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const float4* wn = P.wcopies + oct[k];
+                const uint32_t at = 2u * (go[k] ? ti[k] : root);
+                q0[k] = wn[at];
+                q1[k] = wn[at + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!go[k]) continue;
+                const Ray r{o[k], d[k], rc[k], false, false, false};
+                const bool hit = slab_nf_within(r, q0[k].x, q0[k].y, q0[k].z, q0[k].w, q1[k].x, q1[k].y, bnd[k]);
+                const int tri = f2i(q1[k].w);
+                ti[k] = (hit && tri < 0) ? ti[k] + 1u : (uint32_t)f2i(q1[k].z);
+                if (hit && tri >= 0) {
+                    if (p0[k] < 0) p0[k] = tri;
+                    else p1[k] = tri;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            for (int slot = 0; slot < 2; ++slot) {
+                const int pk = slot == 0 ? p0[k] : p1[k];
+                if (pk < 0) continue;
+                const float4 t0 = P.tris[4 * pk], t1 = P.tris[4 * pk + 1], t2 = P.tris[4 * pk + 2];
+                double t;
+                if (moller_trumbore_od(V3{t0.x, t0.y, t0.z}, V3{t1.x, t1.y, t1.z}, V3{t2.x, t2.y, t2.z}, o[k], d[k], t))
+                    if (t < tA[k] || (t == tA[k] && (uint32_t)pk > (uint32_t)triA[k])) { tA[k] = t; triA[k] = pk; }
+            }
+            if (id[k] != 0xFFFFFFFFu && ti[k] >= tend) {   // done: its result out, the slot free
+                tri_out[id[k]] = triA[k];
+                t_out[id[k]] = triA[k] >= 0 ? tA[k] : 1.7976931348623157e308;
+                id[k] = 0xFFFFFFFFu;
+                ti[k] = NN;
+            }
+        }
+    }
+}
+
+hipError_t rt_launch_walk_study(const KParams& P, uint32_t n, uint32_t k, const float* org, const float* dir, int32_t* tri, double* t, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    const uint32_t kk = k & 0xFFu, waves = (n + 64u * kk - 1u) / (64u * kk), grid = (waves + 3u) / 4u;
+    if (k & 0x100u) {   // refill: a persistent grid of 8 waves per SIMD (256 CUs x 4 SIMDs x 8 / 4 waves per block)
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(P.counters);   // 8 counters, 64 B apart (zeroed by the caller)
+        const uint32_t g = 256u * 8u;
+        switch (k & 0xFFu) {
+        case 1: hipLaunchKernelGGL(walk_study_refill_kernel<1>, dim3(g), dim3(256), 0, stream, P, n, org, dir, tri, t, ctr); break;
+        case 2: hipLaunchKernelGGL(walk_study_refill_kernel<2>, dim3(g), dim3(256), 0, stream, P, n, org, dir, tri, t, ctr); break;
+        case 3: hipLaunchKernelGGL(walk_study_refill_kernel<3>, dim3(g), dim3(256), 0, stream, P, n, org, dir, tri, t, ctr); break;
+        case 4: hipLaunchKernelGGL(walk_study_refill_kernel<4>, dim3(g), dim3(256), 0, stream, P, n, org, dir, tri, t, ctr); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+    if (k == 0x201u) {   // the round count (K = 1, lockstep; a ray's rounds do not depend on the kernel's mode)
+        hipLaunchKernelGGL((walk_study_kernel<1, true>), dim3(grid * 1u), dim3(256), 0, stream, P, n, org, dir, tri, t);
+        return hipGetLastError();
+    }
+    switch (k) {
+    case 1: hipLaunchKernelGGL(walk_study_kernel<1>, dim3(grid), dim3(256), 0, stream, P, n, org, dir, tri, t); break;
+    case 2: hipLaunchKernelGGL(walk_study_kernel<2>, dim3(grid), dim3(256), 0, stream, P, n, org, dir, tri, t); break;
+    case 3: hipLaunchKernelGGL(walk_study_kernel<3>, dim3(grid), dim3(256), 0, stream, P, n, org, dir, tri, t); break;
+    case 4: hipLaunchKernelGGL(walk_study_kernel<4>, dim3(grid), dim3(256), 0, stream, P, n, org, dir, tri, t); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#endif

@@ -3,7 +3,7 @@ timing diagnostics (RT_SECTIONS=1 and the candidate-histogram level 3, tools/pro
 waves-per-SIMD settings measured in DESIGN.md 6.4, the round-4 A/B switches (the drain without the pending
 fold, the BVH variant's division kind, the zero-numerator short division) and the round-6 ones (the C5 A + B pair walk,
 the walk fallback with the sphere branch; in rt_whitted.hip the shadow-ray pair walk, the half-plane orderings and
-the packet walk).  The product build is the Makefile's; these compile
+the packet walk; in rt_kernels.hip the walk study's K-rays-per-lane kernel, tools/walk_study.py).  The product build is the Makefile's; these compile
 rt_coherent.hip alone, device code only, so a diagnostic that is not built by default cannot rot."""
 import os
 import shutil
@@ -21,7 +21,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
                                    "-DRT_PEND_FOLD=0 -DRT_COH_BVH_PRE_MIN_WAVES=8",
                                    "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0", "-DRT_BVH_PAIR=1 -DRT_COH_SPH=1", "-DRT_MT_LOOP32=0 -DRT_B_TOP_FIRST=1 -DRT_MT_PK=1",
                                    "@rt_whitted.hip -DRT_WH_PAIR=1 -DRT_WH_WAVES=6", "@rt_whitted.hip -DRT_WH_HALF=1",
-                                   "@rt_whitted.hip -DRT_WH_PACKET=1"])
+                                   "@rt_whitted.hip -DRT_WH_PACKET=1", "@rt_kernels.hip -DRT_WALK_STUDY=1"])
 def test_coherent_kernel_variant_compiles(flags, tmp_path):
     cmd = [HIPCC, "-std=c++20", "-O3", "-I" + os.path.join(REPO, "include"), "-I" + os.path.join(PKG, "csrc"), "-ffp-contract=off",
            "-fno-fast-math", "--offload-arch=gfx950", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
