@@ -289,6 +289,12 @@ __device__ __forceinline__ bool finite3(V3 v) { return __builtin_isfinite(v.x) &
 // the leaf-box variant's candidate loop over two 32-bit masks (ray A's, then ray B's) instead of one 64-bit mask:
 // 32-bit scans and clears, no 64-bit add; C4 +0.6 % / +0.5 % (both orders), C2 +0.7 %, bitwise
 // (profiles/r06/ab/ab_c{4,2}_mt_loop32*.json)
+// the BVH variant's split-phase candidate loop over two 32-bit masks (ray A's outside slots, then ray B's) instead of one
+// 64-bit mask, as RT_MT_LOOP32 below: C5 3840x2160x32 path kernel 40.61 -> 40.35 ms and 40.52 -> 40.39 ms in the two A/B
+// orders, bitwise (profiles/r06/ab/ab_c5_split_loop32*.json)
+#ifndef RT_SPLIT_LOOP32
+#define RT_SPLIT_LOOP32 1
+#endif
 #ifndef RT_MT_LOOP32
 #define RT_MT_LOOP32 1
 #endif
@@ -1314,11 +1320,23 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                     const uint32_t code = (lsu(VS_MAT) >> VS_SKIP_SHIFT) & 31u;
                     const uint32_t bskip = code != 0u ? __float_as_uint(S.ltris[4 * (code - 1u)].w) : 0u;
                     mb = okB ? mb & ~bskip : 0u;
+#if RT_SPLIT_LOOP32
+                    // two 32-bit masks (ray A's slots, then ray B's), as the leaf-box variant's candidate loop
+                    uint32_t am = ma, bm = mb;
+                    while ((am | bm) != 0u) {
+                        const bool useA = am != 0u;
+                        const uint32_t m = useA ? am : bm;
+                        const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                        const uint32_t mn = m & (m - 1u);
+                        if (useA) am = mn;
+                        else bm = mn;
+#else
                     uint64_t cm = (uint64_t)ma | ((uint64_t)mb << 32);
                     while (cm != 0) {
                         const uint32_t bit = (uint32_t)__builtin_ctzll(cm);
                         cm &= cm - 1;
                         const bool useA = bit < 32u;
+#endif
                         // the slot's triangle, staged in LDS after the small tables (a, e1, (e2, bits(triangle)))
                         const float4* T = lds_scene + (2u * kargs4().n_mats + kargs4().n_lnodes + 4u * kargs4().n_ltris) + 3u * (bit & 31u);
                         const float4 t0 = T[0], t1 = T[1], t2 = T[2];
@@ -1330,7 +1348,11 @@ __global__ void __launch_bounds__(256, BVH ? (PREPASS ? RT_COH_BVH_PRE_MIN_WAVES
                             } else if (!((double)slen < t + (double)0.01f)) {   // MC/Renderer.cpp:184
                                 occB = true;
                                 nB = NN;
+#if RT_SPLIT_LOOP32
+                                bm = 0u;   // nothing else to test
+#else
                                 cm = 0;   // ray B's candidates come last
+#endif
                             }
                         }
                     }

@@ -19,7 +19,7 @@ HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("flags", ["-DRT_SECTIONS=1", "-DRT_SECTIONS=3", "-DRT_COH_MIN_WAVES=7 -DRT_COH_BVH_MIN_WAVES=7",
                                    "-DRT_PEND_FOLD=0 -DRT_COH_BVH_PRE_MIN_WAVES=8",
-                                   "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0", "-DRT_BVH_PAIR=1 -DRT_COH_SPH=1", "-DRT_MT_LOOP32=0 -DRT_B_TOP_FIRST=1 -DRT_MT_PK=1",
+                                   "-DRT_BVH_DIV_FAST=1 -DRT_DIV_ZERO_FAST=0", "-DRT_BVH_PAIR=1 -DRT_COH_SPH=1", "-DRT_MT_LOOP32=0 -DRT_B_TOP_FIRST=1 -DRT_MT_PK=1 -DRT_SPLIT_LOOP32=0",
                                    "@rt_whitted.hip -DRT_WH_PAIR=1 -DRT_WH_WAVES=6", "@rt_whitted.hip -DRT_WH_HALF=1",
                                    "@rt_whitted.hip -DRT_WH_PACKET=1", "@rt_kernels.hip -DRT_WALK_STUDY=1"])
 def test_coherent_kernel_variant_compiles(flags, tmp_path):
