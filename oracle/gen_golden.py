@@ -19,6 +19,7 @@ Container-only (needs /root/reference); the GPU box uses the committed fixtures.
     python oracle/gen_golden.py full_c5_4096  # C5 at its full 4096 spp, every 64th row (~10 min)
     python oracle/gen_golden.py full_c5_4096_mid  # the same frame's rows 32, 96, ... (round 6)
     python oracle/gen_golden.py full_c5_4096_o16  # ... rows 16, 80, ...; full_c5_4096_o48: rows 48, 112, ... (round 6)
+    python oracle/gen_golden.py full_c5_4096_o8   # ... rows 8, 72, ...; _o24, _o40, _o56 likewise (round 6: every 8th row)
 """
 import os
 import subprocess
@@ -741,9 +742,10 @@ def main():
             gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE)
         if only == "full_c5_4096_mid":
             gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=C5_FULL_ROW_STRIDE // 2)
-        if only in ("full_c5_4096_o16", "full_c5_4096_o48"):
-            # the rows a quarter of the stride off (16, 80, ... and 48, 112, ...): with full_c5_4096 and _mid, every 16th row
-            gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=int(only[-2:]))
+        if only.startswith("full_c5_4096_o"):
+            # the rows off by 16 / 48 (16, 80, ... and 48, 112, ...): with full_c5_4096 and _mid, every 16th row; by 8, 24,
+            # 40, 56 as well (full_c5_4096_o8 ...): every 8th row
+            gen_full_c5(4096, row_stride=C5_FULL_ROW_STRIDE, row_offset=int(only[len("full_c5_4096_o"):]))
     print("golden fixtures written to", GOLDEN)
 
 

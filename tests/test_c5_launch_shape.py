@@ -14,7 +14,8 @@ the SHA-256 of the float4 accumulation and of the RGBA8 frame, and every 64th ac
 tests/golden/full_c5_4096.npz is the same at C5's full 4096 spp on every 64th row (`gen_golden.py full_c5_4096`:
 the harness renders only those rows -- the whole frame would take ~11 h on 8 cores); its SHA-256 covers those
 rows.  tests/golden/full_c5_4096_mid.npz, _o16.npz and _o48.npz (round 6) hold the rows 32, 96, ..., 16, 80, ... and
-48, 112, ..., so the 4096-spp frame is pinned on every 16th row.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
+48, 112, ..., so the 4096-spp frame is pinned on every 16th row; _o8, _o24, _o40 and _o56 (late round 6) the rows
+8, 24, 40 and 56 off, every 8th row with all of them.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
 the default budget) and compares the rows of both."""
 import hashlib
 import os
@@ -26,8 +27,10 @@ import _oracle as O
 from _rt import rt
 
 FIXTURES = [n for n in ("full_c5", "full_c5_4096") if os.path.exists(os.path.join(O.GOLDEN, f"{n}.npz"))]
-EXTRA_4096 = ("full_c5_4096_mid", "full_c5_4096_o16", "full_c5_4096_o48")
-ROW_OFFSET = {"full_c5_4096_mid": 32, "full_c5_4096_o16": 16, "full_c5_4096_o48": 48}
+EXTRA_4096 = ("full_c5_4096_mid", "full_c5_4096_o16", "full_c5_4096_o48", "full_c5_4096_o8", "full_c5_4096_o24", "full_c5_4096_o40",
+              "full_c5_4096_o56")
+ROW_OFFSET = {"full_c5_4096_mid": 32, "full_c5_4096_o16": 16, "full_c5_4096_o48": 48, "full_c5_4096_o8": 8, "full_c5_4096_o24": 24,
+              "full_c5_4096_o40": 40, "full_c5_4096_o56": 56}
 
 
 def bits(a):
@@ -106,7 +109,7 @@ def test_c5_frame_in_launch_shape(scene, monkeypatch, name, budget_mb, min_passe
         c.close()
     zs = [z]
     if name == "full_c5_4096":
-        # the same frame's rows 32, 96, ... and 16, 80, ... / 48, 112, ... (round 6): every 16th row
+        # the same frame's rows 32, 96, ..., 16, 80, ... / 48, 112, ... and 8 / 24 / 40 / 56 off (round 6): every 8th row
         zs += [np.load(os.path.join(O.GOLDEN, f"{x}.npz")) for x in EXTRA_4096 if os.path.exists(os.path.join(O.GOLDEN, f"{x}.npz"))]
     for z in zs:
         rows = acc[z["rows"], :, :3]
