@@ -378,7 +378,8 @@ def c5_config(rt, dev_index, stream, spp, fast):
                       "sha_accum_match": sha, "sha_match": bool(sha and same.all())}
             # the same frame's other row sets (round 6): rows 32, 96, ... (_mid), 16, 80, ... (_o16), 48, 112, ... (_o48), and
             # 8, 24, 40, 56 off (_o8 ... _o56): with all of them every 8th row
-            extra = [x for x in ("_mid", "_o16", "_o48", "_o8", "_o24", "_o40", "_o56")
+            # (and 4, 12, ..., 60 off: every 4th row)
+            extra = [x for x in ("_mid", "_o16", "_o48", "_o8", "_o24", "_o40", "_o56") + tuple(f"_o{o}" for o in range(4, 64, 8))
                      if os.path.exists(os.path.join(REPO, "tests", "golden", f"{name}{x}.npz"))]
             if extra:
                 same_all, n_rows, sha_all = [same.ravel()], len(rows), sha
@@ -392,7 +393,7 @@ def c5_config(rt, dev_index, stream, spp, fast):
                     n_rows += len(zm["rows"])
                 same_all = np.concatenate(same_all)
                 parity.update({"fixture": f"tests/golden/{name}.npz" + "".join(f" + {name}{x}.npz" for x in extra), "rows_checked": int(n_rows),
-                               "scope": f"every {64 // (1 + len(extra))}th row" if len(extra) in (1, 3, 7) else f"{n_rows} rows",
+                               "scope": f"every {64 // (1 + len(extra))}th row" if len(extra) in (1, 3, 7, 15) else f"{n_rows} rows",
                                "rmse_vs_ref": float(np.sqrt(np.mean((ca - cb) ** 2))),
                                "bitwise_frac": round(float(same_all.mean()), 6), "sha_accum_match": bool(sha_all),
                                "sha_match": bool(sha_all and same_all.all())})

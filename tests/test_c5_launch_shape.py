@@ -28,9 +28,8 @@ from _rt import rt
 
 FIXTURES = [n for n in ("full_c5", "full_c5_4096") if os.path.exists(os.path.join(O.GOLDEN, f"{n}.npz"))]
 EXTRA_4096 = ("full_c5_4096_mid", "full_c5_4096_o16", "full_c5_4096_o48", "full_c5_4096_o8", "full_c5_4096_o24", "full_c5_4096_o40",
-              "full_c5_4096_o56")
-ROW_OFFSET = {"full_c5_4096_mid": 32, "full_c5_4096_o16": 16, "full_c5_4096_o48": 48, "full_c5_4096_o8": 8, "full_c5_4096_o24": 24,
-              "full_c5_4096_o40": 40, "full_c5_4096_o56": 56}
+              "full_c5_4096_o56") + tuple(f"full_c5_4096_o{o}" for o in range(4, 64, 8))
+ROW_OFFSET = {"full_c5_4096_mid": 32, **{f"full_c5_4096_o{o}": o for o in range(4, 64, 4) if o != 32}}
 
 
 def bits(a):
