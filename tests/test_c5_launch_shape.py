@@ -15,7 +15,7 @@ tests/golden/full_c5_4096.npz is the same at C5's full 4096 spp on every 64th ro
 the harness renders only those rows -- the whole frame would take ~11 h on 8 cores); its SHA-256 covers those
 rows.  tests/golden/full_c5_4096_mid.npz, _o16.npz and _o48.npz (round 6) hold the rows 32, 96, ..., 16, 80, ... and
 48, 112, ..., so the 4096-spp frame is pinned on every 16th row; _o8, _o24, _o40 and _o56 (late round 6) the rows
-8, 24, 40 and 56 off, every 8th row with all of them.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
+8, 24, 40 and 56 off, every 8th row with all of them; _o4, _o12, ..., _o60 the rows 4 off those, every 4th row.  The GPU renders the whole frame in the benchmark's launch shape (ten passes at
 the default budget) and compares the rows of both."""
 import hashlib
 import os
@@ -108,7 +108,7 @@ def test_c5_frame_in_launch_shape(scene, monkeypatch, name, budget_mb, min_passe
         c.close()
     zs = [z]
     if name == "full_c5_4096":
-        # the same frame's rows 32, 96, ..., 16, 80, ... / 48, 112, ... and 8 / 24 / 40 / 56 off (round 6): every 8th row
+        # the same frame's rows 32, 96, ..., 16, 80, ... / 48, 112, ... and 8 / 24 / 40 / 56 and 4 / 12 / ... / 60 off (round 6): every 4th row
         zs += [np.load(os.path.join(O.GOLDEN, f"{x}.npz")) for x in EXTRA_4096 if os.path.exists(os.path.join(O.GOLDEN, f"{x}.npz"))]
     for z in zs:
         rows = acc[z["rows"], :, :3]
